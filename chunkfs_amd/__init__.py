@@ -1,0 +1,241 @@
+"""chunkfs_amd -- MI355X-native content-defined chunking behind chunkfs's Chunker API.
+
+Host-side mirror of the reference's chunking surface, over the C ABI in
+include/chunkfs_amd.h (libchunkfs_amd.so, hand-written HIP for gfx950):
+
+    reference (Rust)                          here
+    Chunk            src/lib.rs:43-66         Chunk
+    Chunker trait    src/lib.rs:74-86         Chunker.chunk_data / estimate_chunk_count
+    SizeParams       src/chunkers/mod.rs:1    SizeParams
+    FastChunker      src/chunkers/fast.rs     FastChunker
+    FSChunker        src/chunkers/fixed_size  FSChunker
+    Rabin/Super/Ultra/Leap/Seq                raise NotImplementedError (no oracle
+                                              offline: cdc-chunkers 0.1.3 absent)
+    ChunkStorage::write  system/storage.rs    write_spans()
+
+Every call runs on the GPU.  There is no CPU fallback: without the built
+library or a gfx950 device the constructors raise.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import ALGO, CdcError, cdc_chunk_t, cdc_timing_t, check, lib
+
+KB = 1024
+MB = 1024 * KB
+GB = 1024 * MB
+SEG_SIZE = MB  # src/lib.rs:39
+
+__all__ = [
+    "KB", "MB", "GB", "SEG_SIZE", "Chunk", "SizeParams", "Chunker", "FastChunker",
+    "FSChunker", "RabinChunker", "SuperChunker", "UltraChunker", "LeapChunker",
+    "SeqChunker", "CdcError", "write_spans", "version",
+]
+
+
+class Chunk:
+    """A chunk of processed data: offset and length only (src/lib.rs:41-66)."""
+
+    __slots__ = ("_offset", "_length")
+
+    def __init__(self, offset, length):
+        self._offset = int(offset)
+        self._length = int(length)
+
+    def offset(self):
+        return self._offset
+
+    def length(self):
+        return self._length
+
+    def range(self):
+        return range(self._offset, self._offset + self._length)
+
+    def __eq__(self, other):
+        return isinstance(other, Chunk) and (self._offset, self._length) == (other._offset, other._length)
+
+    def __hash__(self):
+        return hash((self._offset, self._length))
+
+    def __repr__(self):
+        return f"Chunk {{ offset: {self._offset}, length: {self._length} }}"
+
+
+class SizeParams:
+    """cdc_chunkers::SizeParams {min, avg, max} (re-exported at src/chunkers/mod.rs:1)."""
+
+    __slots__ = ("min", "avg", "max")
+
+    def __init__(self, min, avg, max):  # noqa: A002 -- reference field names
+        self.min, self.avg, self.max = int(min), int(avg), int(max)
+
+    def __repr__(self):
+        return f"SizeParams {{ min: {self.min}, avg: {self.avg}, max: {self.max} }}"
+
+    def __eq__(self, other):
+        return isinstance(other, SizeParams) and (self.min, self.avg, self.max) == (other.min, other.avg, other.max)
+
+
+def _as_buffer(data):
+    """(pointer, length, keepalive) for bytes / bytearray / numpy / memoryview."""
+    if isinstance(data, np.ndarray):
+        arr = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    else:
+        arr = np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+    return arr.ctypes.data_as(ctypes.c_void_p), arr.size, arr
+
+
+class Chunker:
+    """The Chunker trait (src/lib.rs:74-86), backed by one GPU handle.
+
+    Not thread-safe, like the reference's Mutex-serialised ChunkerRef.
+    """
+
+    _algo = None
+
+    def __init__(self, algo, min, avg, max, device=0):  # noqa: A002
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.cdc_create(ALGO[algo], min, avg, max, device, ctypes.byref(h))
+        if rc == -4:
+            raise NotImplementedError(L.cdc_last_error().decode())
+        check(rc)
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().cdc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- trait methods -------------------------------------------------------
+    def chunk_array(self, data):
+        """chunk_data as an (n, 2) uint64 array of (offset, length)."""
+        ptr, n, keep = _as_buffer(data)
+        cap = lib().cdc_max_chunk_count(self._h, n)
+        out = np.empty((max(cap, 1), 2), dtype=np.uint64)
+        cnt = check(lib().cdc_chunk_data(self._h, ptr, n,
+                                         out.ctypes.data_as(ctypes.POINTER(cdc_chunk_t)), cap))
+        del keep
+        assert cnt <= cap
+        return out[:cnt]
+
+    def chunk_data(self, data, empty=None):
+        """Chunker::chunk_data (src/lib.rs:80): chunks tiling `data`, appended to `empty`."""
+        chunks = [] if empty is None else empty
+        chunks.extend(Chunk(int(o), int(l)) for o, l in self.chunk_array(data))
+        return chunks
+
+    def estimate_chunk_count(self, data):
+        """Chunker::estimate_chunk_count (src/lib.rs:85) -- the reference formula."""
+        if isinstance(data, int):
+            n = data
+        elif isinstance(data, np.ndarray):
+            n = data.nbytes
+        else:
+            n = memoryview(data).nbytes
+        return lib().cdc_estimate_chunk_count(self._h, n)
+
+    def max_chunk_count(self, n):
+        return lib().cdc_max_chunk_count(self._h, n)
+
+    def __repr__(self):  # impl Debug
+        return lib().cdc_describe(self._h).decode()
+
+    # -- device-resident batch (configs 2, 4) --------------------------------
+    def chunk_batch_device(self, d_ptrs, lens, d_out_ptr, out_cap, stream=0):
+        """Chunk n streams already in HBM.  Returns the host array first[n+1]."""
+        n = len(lens)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(int(p)) for p in d_ptrs])
+        lens_a = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
+        first = (ctypes.c_uint64 * (n + 1))()
+        check(lib().cdc_chunk_batch_device(self._h, n, ptrs, lens_a, ctypes.c_void_p(int(d_out_ptr)),
+                                           out_cap, first, ctypes.c_void_p(int(stream))))
+        return np.frombuffer(first, dtype=np.uint64).copy()
+
+    def batch_max_chunks(self, lens):
+        n = len(lens)
+        lens_a = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
+        return lib().cdc_batch_max_chunks(self._h, n, lens_a)
+
+    def last_timing(self):
+        t = cdc_timing_t()
+        check(lib().cdc_last_timing(self._h, ctypes.byref(t)))
+        return {f: getattr(t, f) for f, _ in cdc_timing_t._fields_}
+
+    def set_gear(self, gear):
+        g = np.ascontiguousarray(gear, dtype=np.uint64)
+        assert g.shape == (256,)
+        check(lib().cdc_set_gear(self._h, g.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+
+
+class FastChunker(Chunker):
+    """FastCDC 2020 (src/chunkers/fast.rs); default sizes 8/16/64 KiB (fast.rs:17-27)."""
+
+    def __init__(self, sizes=None, device=0):
+        sizes = sizes or SizeParams(8 * KB, 16 * KB, 64 * KB)
+        self.sizes = sizes
+        super().__init__("fast", sizes.min, sizes.avg, sizes.max, device)
+
+    @classmethod
+    def default(cls):
+        return cls()
+
+
+class FSChunker(Chunker):
+    """Fixed-size chunking (src/chunkers/fixed_size.rs); default 4096 (fixed_size.rs:26-30)."""
+
+    def __init__(self, chunk_size=4096, device=0):
+        self.chunk_size = chunk_size
+        super().__init__("fixed", chunk_size, 0, 0, device)
+
+    @classmethod
+    def default(cls):
+        return cls()
+
+
+def _unsupported(name, algo):
+    class _C(Chunker):
+        def __init__(self, sizes=None, device=0):
+            s = sizes or SizeParams(2 * KB, 8 * KB, 64 * KB)
+            super().__init__(algo, s.min, s.avg, s.max, device)
+
+    _C.__name__ = name
+    _C.__doc__ = (f"{name} (src/chunkers/{algo}.rs): not implemented -- its arithmetic lives in "
+                  "cdc-chunkers 0.1.3, absent offline, so no oracle exists (SURVEY.md §8c).")
+    return _C
+
+
+RabinChunker = _unsupported("RabinChunker", "rabin")
+SuperChunker = _unsupported("SuperChunker", "super")
+UltraChunker = _unsupported("UltraChunker", "ultra")
+LeapChunker = _unsupported("LeapChunker", "leap")
+SeqChunker = _unsupported("SeqChunker", "seq")
+
+
+def write_spans(chunker, data, seg_size=SEG_SIZE):
+    """ChunkStorage::write (storage.rs:78-103) for one write call.
+
+    Returns (span lengths in file order, seconds spent inside chunk_data).
+    """
+    ptr, n, keep = _as_buffer(data)
+    cap = chunker.max_chunk_count(n) + 1  # spans are chunks: all but the last are >= min
+    out = np.empty(max(cap, 1), dtype=np.uint64)
+    secs = ctypes.c_double(0.0)
+    cnt = check(lib().cdc_fs_write(chunker._h, ptr, n, seg_size,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap,
+                                   ctypes.byref(secs)))
+    del keep
+    assert cnt <= cap
+    return out[:cnt], secs.value
+
+
+def version():
+    return lib().cdc_version().decode()

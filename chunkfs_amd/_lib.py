@@ -1,0 +1,106 @@
+"""ctypes binding of libchunkfs_amd.so (include/chunkfs_amd.h).
+
+Loading fails loudly: there is no CPU fallback anywhere in the product.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libchunkfs_amd.so")
+
+CDC_OK = 0
+CDC_EINVAL = -1
+CDC_ENOMEM = -2
+CDC_EDEVICE = -3
+CDC_ENOTSUP = -4
+
+ALGO = {"fast": 0, "fixed": 1, "rabin": 2, "super": 3, "ultra": 4, "leap": 5, "seq": 6}
+
+# Every symbol include/chunkfs_amd.h declares (tests check the export table).
+EXPORTS = [
+    "cdc_create", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
+    "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear",
+    "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
+    "cdc_fs_write", "cdc_fill_splitmix64_device", "cdc_version",
+]
+
+
+class CdcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"chunkfs_amd error {code}: {msg}")
+        self.code = code
+
+
+class cdc_chunk_t(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint64)]
+
+
+class cdc_timing_t(ctypes.Structure):
+    _fields_ = [
+        ("scan_ms", ctypes.c_double),
+        ("resolve_ms", ctypes.c_double),
+        ("compact_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
+        ("fixup_iterations", ctypes.c_uint32),
+        ("overflow_spans", ctypes.c_uint32),
+        ("candidates", ctypes.c_uint64),
+        ("bytes", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load and type the shared library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP engine is the only implementation; there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    sz = ctypes.c_size_t
+    L.cdc_create.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                             ctypes.c_int, ctypes.POINTER(P)]
+    L.cdc_create.restype = ctypes.c_int
+    L.cdc_destroy.argtypes = [P]
+    L.cdc_destroy.restype = None
+    L.cdc_chunk_data.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), sz]
+    L.cdc_chunk_data.restype = ctypes.c_int64
+    L.cdc_estimate_chunk_count.argtypes = [P, sz]
+    L.cdc_estimate_chunk_count.restype = sz
+    L.cdc_max_chunk_count.argtypes = [P, sz]
+    L.cdc_max_chunk_count.restype = sz
+    L.cdc_describe.argtypes = [P]
+    L.cdc_describe.restype = ctypes.c_char_p
+    L.cdc_last_error.argtypes = []
+    L.cdc_last_error.restype = ctypes.c_char_p
+    L.cdc_set_gear.argtypes = [P, u64p]
+    L.cdc_set_gear.restype = ctypes.c_int
+    L.cdc_chunk_batch_device.argtypes = [P, sz, ctypes.POINTER(P), u64p, P, sz, u64p, P]
+    L.cdc_chunk_batch_device.restype = ctypes.c_int64
+    L.cdc_batch_max_chunks.argtypes = [P, sz, u64p]
+    L.cdc_batch_max_chunks.restype = sz
+    L.cdc_last_timing.argtypes = [P, ctypes.POINTER(cdc_timing_t)]
+    L.cdc_last_timing.restype = ctypes.c_int
+    L.cdc_fs_write.argtypes = [P, P, sz, sz, u64p, sz, ctypes.POINTER(ctypes.c_double)]
+    L.cdc_fs_write.restype = ctypes.c_int64
+    L.cdc_fill_splitmix64_device.argtypes = [P, sz, ctypes.c_uint64, P]
+    L.cdc_fill_splitmix64_device.restype = ctypes.c_int
+    L.cdc_version.argtypes = []
+    L.cdc_version.restype = ctypes.c_char_p
+    del u8p
+    _lib = L
+    return L
+
+
+def check(rc):
+    """Raise CdcError for a negative return code, else return rc."""
+    if rc < 0:
+        raise CdcError(rc, lib().cdc_last_error().decode())
+    return rc

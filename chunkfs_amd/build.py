@@ -1,0 +1,53 @@
+"""In-tree build of libchunkfs_amd.so for gfx950 (hipcc cross-compiles without a GPU).
+
+The .so is git-ignored but travels to the GPU box with the gpurun snapshot.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libchunkfs_amd.so")
+SOURCES = ["cdc_kernels.hip", "engine.cpp", "capi.cpp"]
+HEADERS = ["cdc_kernels.hpp", "engine.hpp", "storage_writer.hpp"]
+ARCH = "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def build(force=False):
+    os.makedirs(BUILD, exist_ok=True)
+    common = [os.path.join(CSRC, h) for h in HEADERS] + [
+        os.path.join(ROOT, "include", "chunkfs_amd.h"),
+        os.path.join(ROOT, "include", "chunkfs_amd_tables.h"),
+    ]
+    objs = []
+    for src in SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(BUILD, src + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + common):
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            _run([HIPCC] + CFLAGS + lang + ["-c", s, "-o", o])
+    if force or _newer(LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

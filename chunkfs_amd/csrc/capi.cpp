@@ -1,0 +1,121 @@
+// capi.cpp -- extern "C" entry points of libchunkfs_amd.so (include/chunkfs_amd.h).
+#include <string>
+#include <vector>
+
+#include "../../include/chunkfs_amd.h"
+#include "engine.hpp"
+#include "storage_writer.hpp"
+
+struct cdc_handle {
+    cdc::Engine *engine;
+};
+
+namespace {
+int64_t bad_handle() {
+    cdc::set_error("NULL handle");
+    return CDC_EINVAL;
+}
+}  // namespace
+
+extern "C" {
+
+int cdc_create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
+               int device, cdc_handle_t **out) {
+    cdc::Engine *e = nullptr;
+    const int rc = cdc::Engine::create(algo, min, avg, max, device, &e);
+    if (rc != CDC_OK) return rc;
+    *out = new cdc_handle{e};
+    return CDC_OK;
+}
+
+void cdc_destroy(cdc_handle_t *h) {
+    if (!h) return;
+    delete h->engine;
+    delete h;
+}
+
+int64_t cdc_chunk_data(cdc_handle_t *h, const uint8_t *data, size_t len,
+                       cdc_chunk_t *out, size_t cap) {
+    if (!h) return bad_handle();
+    return h->engine->chunk_host(data, len, out, cap);
+}
+
+size_t cdc_estimate_chunk_count(const cdc_handle_t *h, size_t len) {
+    return h ? h->engine->estimate(len) : 0;
+}
+
+size_t cdc_max_chunk_count(const cdc_handle_t *h, size_t len) {
+    return h ? h->engine->max_chunks(len) : 0;
+}
+
+const char *cdc_describe(const cdc_handle_t *h) {
+    return h ? h->engine->describe() : "";
+}
+
+const char *cdc_last_error(void) { return cdc::last_error(); }
+
+int cdc_set_gear(cdc_handle_t *h, const uint64_t gear[256]) {
+    if (!h) return (int)bad_handle();
+    return h->engine->set_gear(gear);
+}
+
+int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
+                               const uint8_t *const *d_streams,
+                               const uint64_t *lens, cdc_chunk_t *d_out,
+                               size_t out_cap, uint64_t *first,
+                               void *hip_stream) {
+    if (!h) return bad_handle();
+    return h->engine->chunk_batch_device(n, d_streams, lens, d_out, out_cap, first,
+                                         static_cast<hipStream_t>(hip_stream));
+}
+
+size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n, const uint64_t *lens) {
+    return (h && lens) ? h->engine->batch_max_chunks(n, lens) : 0;
+}
+
+int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t) {
+    if (!h || !t) return (int)bad_handle();
+    *t = h->engine->timing();
+    return CDC_OK;
+}
+
+int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
+                     size_t seg_size, uint64_t *span_lengths, size_t cap,
+                     double *chunk_seconds) {
+    if (!h) return bad_handle();
+    if (len && !data) {
+        cdc::set_error("cdc_fs_write: data is NULL");
+        return CDC_EINVAL;
+    }
+    cdc::Engine *e = h->engine;
+    auto chunk = [e](const uint8_t *buf, size_t n, std::vector<cdc_chunk_t> &out) -> int64_t {
+        out.resize(e->max_chunks(n));
+        const int64_t c = e->chunk_host(buf, n, out.data(), out.size());
+        if (c >= 0) out.resize((size_t)c);
+        return c;
+    };
+    std::vector<uint64_t> spans;
+    const int64_t n = cdc::storage_write_spans(chunk, data, len, seg_size, spans, chunk_seconds);
+    if (n < 0) return n;
+    for (size_t i = 0; i < spans.size() && i < cap; ++i) span_lengths[i] = spans[i];
+    return n;
+}
+
+int cdc_fill_splitmix64_device(uint8_t *d_buf, size_t len, uint64_t seed, void *hip_stream) {
+    if (len && !d_buf) {
+        cdc::set_error("NULL buffer");
+        return CDC_EINVAL;
+    }
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    hipError_t e = cdc::launch_fill_splitmix64(d_buf, len, seed, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        cdc::set_error(std::string("fill: ") + hipGetErrorString(e));
+        return CDC_EDEVICE;
+    }
+    return CDC_OK;
+}
+
+const char *cdc_version(void) { return "chunkfs_amd 0.1 gfx950 abi 1"; }
+
+}  // extern "C"

@@ -1,0 +1,447 @@
+// engine.cpp -- host orchestration of the gfx950 chunking pipeline.
+//
+// Per batch (DESIGN.md "Pipeline"):
+//   H2D of three tiny per-stream tables -> scan -> spec -> fixup (Jacobi,
+//   until no span exit changes; one flag readback per pass) -> compact ->
+//   D2H of the n+1 per-stream chunk indices.
+// Everything runs on one HIP stream; the candidate lists, chains and output
+// never leave HBM.
+#include "engine.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/chunkfs_amd_tables.h"
+
+namespace cdc {
+
+namespace {
+thread_local std::string g_last_error;
+
+constexpr uint32_t kMinSpanLog2 = 16;  // 64 KiB spans at least
+
+// fastcdc 3.1.0 v2020 FastCDC::new asserts (VERIFY).
+constexpr uint32_t kMinimumMin = 64, kMinimumMax = 1048576;
+constexpr uint32_t kAverageMin = 256, kAverageMax = 4194304;
+constexpr uint32_t kMaximumMin = 1024, kMaximumMax = 16777216;
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+uint32_t ceil_log2(uint64_t x) {
+    uint32_t r = 0;
+    while ((1ull << r) < x) ++r;
+    return r;
+}
+}  // namespace
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+const char *last_error() { return g_last_error.c_str(); }
+
+#define HIP_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));      \
+            return CDC_EDEVICE;                                                \
+        }                                                                      \
+    } while (0)
+
+int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
+                   int device, Engine **out) {
+    if (!out) {
+        set_error("cdc_create: out is NULL");
+        return CDC_EINVAL;
+    }
+    *out = nullptr;
+    if (algo != CDC_ALGO_FASTCDC && algo != CDC_ALGO_FIXED) {
+        set_error("algorithm not implemented on MI355X: its reference arithmetic "
+                  "lives in cdc-chunkers 0.1.3, absent offline (SURVEY.md §8c)");
+        return CDC_ENOTSUP;
+    }
+    Engine *e = new Engine();
+    e->algo_ = algo;
+    e->min_ = min;
+    e->avg_ = avg;
+    e->max_ = max;
+    e->device_ = device;
+    if (algo == CDC_ALGO_FASTCDC) {
+        if (min < kMinimumMin || min > kMinimumMax || avg < kAverageMin ||
+            avg > kAverageMax || max < kMaximumMin || max > kMaximumMax) {
+            set_error("FastCDC sizes out of range (fastcdc v2020 asserts: min 64..1MiB, "
+                      "avg 256..4MiB, max 1KiB..16MiB)");
+            delete e;
+            return CDC_EINVAL;
+        }
+        const unsigned bits = (unsigned)std::lround(std::log2((double)avg));
+        FastParams &fp = e->fp_;
+        fp.min = min;
+        fp.avg = avg;
+        fp.max = max;
+        fp.mask_s = CHUNKFS_AMD_MASKS[bits + 1];
+        fp.mask_l = CHUNKFS_AMD_MASKS[bits - 1];
+        fp.cmask = fp.mask_s & fp.mask_l;
+        const uint64_t all = fp.mask_s | fp.mask_l;
+        const uint32_t top = 63 - (uint32_t)__builtin_clzll(all);
+        if (top > 47) {  // the 3-lane carry is exact mod 2^48 only
+            set_error("mask tests bit >= 48: unsupported");
+            delete e;
+            return CDC_EINVAL;
+        }
+        fp.trunc = top;
+        const uint32_t sh = (uint32_t)__builtin_ctzll(fp.cmask);
+        fp.cm_align = (sh < 32 && (fp.cmask >> sh) <= 0xFFFFFFFFull) ? 1u : 0u;
+        fp.cm_shift = sh < 32 ? sh : 0;
+        fp.cm32 = (uint32_t)(fp.cmask >> fp.cm_shift);
+        fp.cm_lo = (uint32_t)fp.cmask;
+        fp.cm_hi = (uint32_t)(fp.cmask >> 32);
+        uint32_t l2 = ceil_log2(max);
+        e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
+        const uint64_t span = 1ull << e->span_log2_;
+        const uint32_t pc = (uint32_t)__builtin_popcountll(fp.cmask);
+        uint64_t cap = 8 * (span >> (pc < 63 ? pc : 63));
+        if (cap < 64) cap = 64;
+        if (cap > span) cap = span;
+        e->cap_ = (uint32_t)cap;
+        e->smax_ = (uint32_t)(span / ((min / 2) * 2) + 2);
+        char buf[256];
+        std::snprintf(buf, sizeof buf,
+                      "FastCDC (2020), sizes: SizeParams { min: %u, avg: %u, max: %u } "
+                      "[MI355X gfx950]",
+                      min, avg, max);
+        e->describe_ = buf;
+    } else {
+        if (min == 0) {
+            set_error("FSChunker chunk size must be > 0");
+            delete e;
+            return CDC_EINVAL;
+        }
+        char buf[128];
+        std::snprintf(buf, sizeof buf, "Fixed size chunking, chunk size: %u [MI355X gfx950]", min);
+        e->describe_ = buf;
+    }
+    const int rc = e->init();
+    if (rc != CDC_OK) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return CDC_OK;
+}
+
+int Engine::init() {
+    int count = 0;
+    HIP_TRY(hipGetDeviceCount(&count));
+    if (device_ < 0 || device_ >= count) {
+        set_error("device index out of range");
+        return CDC_EDEVICE;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device_));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("chunkfs_amd kernels are built for gfx950 only; device is ") +
+                  prop.gcnArchName);
+        return CDC_EDEVICE;
+    }
+    num_cus_ = prop.multiProcessorCount;
+    HIP_TRY(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking));
+    for (auto &ev : ev_) HIP_TRY(hipEventCreate(&ev));
+    HIP_TRY(hipMalloc(&d_gear_, 256 * sizeof(uint64_t)));
+    HIP_TRY(hipMemcpy(d_gear_, CHUNKFS_AMD_GEAR, 256 * sizeof(uint64_t), hipMemcpyHostToDevice));
+    return CDC_OK;
+}
+
+Engine::~Engine() {
+    if (device_ >= 0) (void)hipSetDevice(device_);
+    if (own_stream_) (void)hipStreamSynchronize(own_stream_);
+    (void)hipFree(ws_);
+    (void)hipFree(d_gear_);
+    (void)hipFree(d_data_);
+    (void)hipFree(d_out_);
+    (void)hipHostFree(h_stage_);
+    for (auto &ev : ev_)
+        if (ev) (void)hipEventDestroy(ev);
+    if (own_stream_) (void)hipStreamDestroy(own_stream_);
+}
+
+int Engine::set_gear(const uint64_t *gear) {
+    if (!gear) {
+        set_error("gear is NULL");
+        return CDC_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    HIP_TRY(hipMemcpy(d_gear_, gear, 256 * sizeof(uint64_t), hipMemcpyHostToDevice));
+    return CDC_OK;
+}
+
+size_t Engine::estimate(size_t len) const {
+    if (algo_ == CDC_ALGO_FIXED) return len / min_ + 1;  // fixed_size.rs:45-47
+    return len / min_;                                   // fast.rs:47-49
+}
+
+size_t Engine::batch_max_chunks(size_t n, const uint64_t *lens) const {
+    size_t t = 0;
+    for (size_t i = 0; i < n; ++i) t += lens[i] / min_chunk() + 1;
+    return t;
+}
+
+int Engine::ensure_host_staging(size_t n) {
+    if (h_stage_ && h_stage_streams_ >= n) return CDC_OK;
+    (void)hipHostFree(h_stage_);
+    h_stage_ = nullptr;
+    const size_t want = n + 64;
+    // ptrs[n] lens[n] span_base[n+1] first[n+1] flag stats[2]
+    HIP_TRY(hipHostMalloc(&h_stage_, (4 * want + 8) * sizeof(uint64_t)));
+    h_stage_streams_ = want;
+    return CDC_OK;
+}
+
+int Engine::ensure_workspace(uint64_t spans, size_t n) {
+    if (ws_ && spans <= ws_spans_ && n <= ws_streams_) return CDC_OK;
+    const uint64_t S = spans > ws_spans_ ? spans + spans / 4 + 16 : ws_spans_;
+    const size_t N = n > ws_streams_ ? n + 64 : ws_streams_;
+    const uint64_t cap = algo_ == CDC_ALGO_FASTCDC ? cap_ : 0;
+    const uint64_t smax = algo_ == CDC_ALGO_FASTCDC ? smax_ : 0;
+    const size_t A = 256;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = align_up(off + bytes, A);
+        return o;
+    };
+    const size_t o_count = take(S * 4), o_pos = take(S * cap * 4), o_hash = take(S * cap * 8);
+    const size_t o_st0 = take(S * smax * 8), o_st1 = take(S * smax * 8);
+    const size_t o_ns0 = take(S * 4), o_ns1 = take(S * 4), o_which = take(S);
+    const size_t o_entry = take(S * 8), o_ex0 = take(S * 8), o_ex1 = take(S * 8);
+    const size_t o_changed = take(8), o_ci = take((S + 1) * 8);
+    const size_t o_bs = take((S / 1024 + 2) * 8), o_stats = take(16), o_first = take((N + 1) * 8);
+    const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
+    (void)hipFree(ws_);
+    ws_ = nullptr;
+    ws_spans_ = 0;
+    ws_streams_ = 0;
+    HIP_TRY(hipMalloc(&ws_, off));
+    ws_bytes_ = off;
+    ws_spans_ = S;
+    ws_streams_ = N;
+    char *b = static_cast<char *>(ws_);
+    cand_.cap = (uint32_t)cap;
+    cand_.count = reinterpret_cast<uint32_t *>(b + o_count);
+    cand_.pos = reinterpret_cast<uint32_t *>(b + o_pos);
+    cand_.hash = reinterpret_cast<uint64_t *>(b + o_hash);
+    chains_.smax = (uint32_t)smax;
+    chains_.starts[0] = reinterpret_cast<uint64_t *>(b + o_st0);
+    chains_.starts[1] = reinterpret_cast<uint64_t *>(b + o_st1);
+    chains_.nstarts[0] = reinterpret_cast<uint32_t *>(b + o_ns0);
+    chains_.nstarts[1] = reinterpret_cast<uint32_t *>(b + o_ns1);
+    chains_.which = reinterpret_cast<uint8_t *>(b + o_which);
+    chains_.entry = reinterpret_cast<uint64_t *>(b + o_entry);
+    chains_.exit[0] = reinterpret_cast<uint64_t *>(b + o_ex0);
+    chains_.exit[1] = reinterpret_cast<uint64_t *>(b + o_ex1);
+    chains_.changed = reinterpret_cast<uint32_t *>(b + o_changed);
+    comp_.chunk_index = reinterpret_cast<uint64_t *>(b + o_ci);
+    comp_.block_sums = reinterpret_cast<uint64_t *>(b + o_bs);
+    comp_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
+    comp_.first = reinterpret_cast<uint64_t *>(b + o_first);
+    d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
+    d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
+    d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
+    return CDC_OK;
+}
+
+int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
+                                   const uint64_t *lens, cdc_chunk_t *d_out,
+                                   size_t out_cap, uint64_t *first,
+                                   hipStream_t stream) {
+    if (n && (!d_streams || !lens || !first)) {
+        set_error("cdc_chunk_batch_device: NULL argument");
+        return CDC_EINVAL;
+    }
+    if (n > 0xFFFFFFFEull) {
+        set_error("too many streams");
+        return CDC_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    hipStream_t s = stream ? stream : own_stream_;
+    timing_ = cdc_timing_t{};
+    uint64_t bytes = 0, need = 0;
+    for (size_t i = 0; i < n; ++i) {
+        bytes += lens[i];
+        need += lens[i] / min_chunk() + 1;
+        if (lens[i] && !d_streams[i]) {
+            set_error("NULL stream pointer with non-zero length");
+            return CDC_EINVAL;
+        }
+        if (lens[i] && algo_ == CDC_ALGO_FASTCDC && (reinterpret_cast<uintptr_t>(d_streams[i]) & 15)) {
+            set_error("device stream pointers must be 16-byte aligned");
+            return CDC_EINVAL;
+        }
+    }
+    timing_.bytes = bytes;
+    if (need > out_cap) {
+        set_error("out_cap < cdc_batch_max_chunks()");
+        return CDC_EINVAL;
+    }
+    if (n == 0) {
+        if (first) first[0] = 0;
+        return 0;
+    }
+    int rc = ensure_host_staging(n);
+    if (rc) return rc;
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
+    const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : 0;
+    uint64_t spans = 0;
+    for (size_t i = 0; i < n; ++i) {
+        h_ptrs[i] = reinterpret_cast<uint64_t>(d_streams[i]);
+        h_lens[i] = lens[i];
+        h_sb[i] = spans;
+        if (algo_ == CDC_ALGO_FASTCDC) spans += (lens[i] + (1ull << sl2) - 1) >> sl2;
+    }
+    h_sb[n] = spans;
+    if (algo_ == CDC_ALGO_FASTCDC && spans == 0) {  // every stream is empty
+        for (size_t i = 0; i <= n; ++i) first[i] = 0;
+        return 0;
+    }
+    rc = ensure_workspace(spans, n);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(d_ptrs_, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_lens_, h_lens, n * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_span_base_, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    StreamTable st{};
+    st.ptrs = d_ptrs_;
+    st.lens = d_lens_;
+    st.span_base = d_span_base_;
+    st.n = (uint32_t)n;
+    st.span_log2 = sl2;
+    st.total_spans = spans;
+    rc = algo_ == CDC_ALGO_FASTCDC ? run_fast(st, d_out, n, first, s)
+                                   : run_fixed(st, n, lens, d_out, first, s);
+    if (rc) return rc;
+    return (int64_t)first[n];
+}
+
+int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+                     uint64_t *first, hipStream_t s) {
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_first = h + 3 * h_stage_streams_;
+    uint64_t *h_misc = h + 4 * h_stage_streams_;  // [0] flag, [1..2] stats
+    HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
+    HIP_TRY(hipEventRecord(ev_[1], s));
+    HIP_TRY(launch_spec(st, fp_, d_gear_, cand_, chains_, s));
+    int b = 0;
+    uint32_t iters = 0;
+    const bool multi = st.total_spans > st.n;  // some stream has >= 2 spans
+    while (multi) {
+        HIP_TRY(hipMemsetAsync(chains_.changed, 0, 4, s));
+        HIP_TRY(launch_fixup(st, fp_, d_gear_, cand_, chains_, b, s));
+        b ^= 1;
+        ++iters;
+        HIP_TRY(hipMemcpyAsync(h_misc, chains_.changed, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (*reinterpret_cast<volatile uint32_t *>(h_misc) == 0) break;
+        if (iters > st.total_spans + 2) {
+            set_error("resolve did not converge (internal error)");
+            return CDC_EDEVICE;
+        }
+    }
+    HIP_TRY(hipEventRecord(ev_[2], s));
+    HIP_TRY(hipMemsetAsync(comp_.stats, 0, 16, s));
+    HIP_TRY(launch_compact(st, chains_, b, cand_, comp_, d_out, s));
+    HIP_TRY(hipMemcpyAsync(h_first, comp_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_misc + 1, comp_.stats, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ev_[3], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(first, h_first, (n + 1) * 8);
+    float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
+    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
+    HIP_TRY(hipEventElapsedTime(&t23, ev_[2], ev_[3]));
+    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
+    timing_.scan_ms = t01;
+    timing_.resolve_ms = t12;
+    timing_.compact_ms = t23;
+    timing_.total_ms = t03;
+    timing_.fixup_iterations = iters;
+    timing_.candidates = h_misc[1];
+    timing_.overflow_spans = (uint32_t)h_misc[2];
+    return CDC_OK;
+}
+
+int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
+                      cdc_chunk_t *d_out, uint64_t *first, hipStream_t s) {
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_first = h + 3 * h_stage_streams_;
+    uint64_t t = 0;
+    for (size_t i = 0; i < n; ++i) {
+        h_first[i] = t;
+        t += (lens[i] + min_ - 1) / min_;  // fixed_size.rs:35-40: ceil(len/cs) chunks
+    }
+    h_first[n] = t;
+    HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(hipMemcpyAsync(comp_.first, h_first, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_fixed(st, min_, comp_.first, d_out, t, s));
+    HIP_TRY(hipEventRecord(ev_[3], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(first, h_first, (n + 1) * 8);
+    float t03 = 0;
+    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
+    timing_.total_ms = t03;
+    timing_.scan_ms = t03;
+    return CDC_OK;
+}
+
+int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out,
+                           size_t cap) {
+    if (len && !data) {
+        set_error("cdc_chunk_data: data is NULL");
+        return CDC_EINVAL;
+    }
+    if (cap && !out) {
+        set_error("cdc_chunk_data: out is NULL");
+        return CDC_EINVAL;
+    }
+    if (len == 0) return 0;  // FastCDC iterator yields nothing; FSChunker loop never runs
+    HIP_TRY(hipSetDevice(device_));
+    if (d_data_bytes_ < len) {
+        (void)hipFree(d_data_);
+        d_data_ = nullptr;
+        d_data_bytes_ = 0;
+        const size_t want = align_up(len + len / 8, 1 << 20);
+        HIP_TRY(hipMalloc(&d_data_, want));
+        d_data_bytes_ = want;
+    }
+    const size_t need = max_chunks(len);
+    if (d_out_cap_ < need) {
+        (void)hipFree(d_out_);
+        d_out_ = nullptr;
+        d_out_cap_ = 0;
+        const size_t want = need + need / 8 + 64;
+        HIP_TRY(hipMalloc(&d_out_, want * sizeof(cdc_chunk_t)));
+        d_out_cap_ = want;
+    }
+    HIP_TRY(hipMemcpyAsync(d_data_, data, len, hipMemcpyHostToDevice, own_stream_));
+    const uint8_t *p = d_data_;
+    const uint64_t l = len;
+    uint64_t first[2] = {0, 0};
+    const int64_t count = chunk_batch_device(1, &p, &l, d_out_, d_out_cap_, first, own_stream_);
+    if (count < 0) return count;
+    const size_t copy = (size_t)count < cap ? (size_t)count : cap;
+    if (copy) {
+        HIP_TRY(hipMemcpyAsync(out, d_out_, copy * sizeof(cdc_chunk_t), hipMemcpyDeviceToHost, own_stream_));
+        HIP_TRY(hipStreamSynchronize(own_stream_));
+    }
+    return count;
+}
+
+int Engine::fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s) {
+    HIP_TRY(hipSetDevice(device_));
+    hipStream_t st = s ? s : own_stream_;
+    HIP_TRY(launch_fill_splitmix64(d_buf, len, seed, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return CDC_OK;
+}
+
+}  // namespace cdc

@@ -1,0 +1,93 @@
+// engine.hpp -- device-side orchestration behind the C ABI.
+//
+// One Engine = one chunker handle bound to one GPU: the FastChunker /
+// FSChunker object of reference src/chunkers/{fast,fixed_size}.rs with its
+// device workspace.  Not thread-safe (the reference serialises through a
+// Mutex, src/lib.rs:89-90).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/chunkfs_amd.h"
+#include "cdc_kernels.hpp"
+
+namespace cdc {
+
+class Engine {
+  public:
+    // Returns CDC_OK or a negative CDC_E* code (message via set_error()).
+    static int create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
+                      int device, Engine **out);
+    ~Engine();
+
+    int64_t chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, size_t cap);
+    int64_t chunk_batch_device(size_t n, const uint8_t *const *d_streams,
+                               const uint64_t *lens, cdc_chunk_t *d_out,
+                               size_t out_cap, uint64_t *first, hipStream_t stream);
+    size_t estimate(size_t len) const;
+    // Strict bound: every FastCDC chunk but the last is >= 2*(min/2) bytes
+    // (cut_gear starts testing at index 2*(min/2)).
+    size_t min_chunk() const { return algo_ == CDC_ALGO_FASTCDC ? (min_ / 2) * 2 : min_; }
+    size_t max_chunks(size_t len) const { return len / min_chunk() + 1; }
+    size_t batch_max_chunks(size_t n, const uint64_t *lens) const;
+    int set_gear(const uint64_t *gear);
+    const char *describe() const { return describe_.c_str(); }
+    const cdc_timing_t &timing() const { return timing_; }
+    cdc_algo_t algo() const { return algo_; }
+    int device() const { return device_; }
+    int fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s);
+
+  private:
+    Engine() = default;
+    int init();
+    int ensure_workspace(uint64_t spans, size_t n);
+    int ensure_host_staging(size_t n);
+    int run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+                 uint64_t *first, hipStream_t s);
+    int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
+                  cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
+
+    cdc_algo_t algo_ = CDC_ALGO_FASTCDC;
+    uint32_t min_ = 0, avg_ = 0, max_ = 0;
+    int device_ = 0;
+    int num_cus_ = 256;
+    FastParams fp_{};
+    uint32_t span_log2_ = 16;
+    uint32_t cap_ = 0, smax_ = 0;
+    std::string describe_;
+
+    hipStream_t own_stream_ = nullptr;
+    hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t *d_gear_ = nullptr;
+
+    // Workspace arena (grow-only).
+    void *ws_ = nullptr;
+    size_t ws_bytes_ = 0;
+    uint64_t ws_spans_ = 0;
+    size_t ws_streams_ = 0;
+    Candidates cand_{};
+    Chains chains_{};
+    Compact comp_{};
+    const uint8_t **d_ptrs_ = nullptr;
+    uint64_t *d_lens_ = nullptr;
+    uint64_t *d_span_base_ = nullptr;
+
+    // Pinned host staging for the small per-call tables.
+    void *h_stage_ = nullptr;
+    size_t h_stage_streams_ = 0;
+
+    // Host-path buffers (cdc_chunk_data).
+    uint8_t *d_data_ = nullptr;
+    size_t d_data_bytes_ = 0;
+    cdc_chunk_t *d_out_ = nullptr;
+    size_t d_out_cap_ = 0;
+
+    cdc_timing_t timing_{};
+};
+
+void set_error(const std::string &msg);
+const char *last_error();
+
+}  // namespace cdc

@@ -1,0 +1,157 @@
+/*
+ * chunkfs_amd.h -- C ABI of the MI355X content-defined-chunking engine.
+ *
+ * This is the drop-in boundary for chunkfs's chunking hot path,
+ * `Chunker::chunk_data` (reference src/lib.rs:74-86).  Every entry point below
+ * names the reference item it replaces.  The signatures use plain pointers and
+ * sizes only, so a Rust `impl Chunker`, ctypes or any other FFI
+ * can bind them.
+ *
+ * Threading: one handle is NOT thread-safe (the reference serialises all calls
+ * through ChunkerRef = Arc<Mutex<dyn Chunker>>, src/lib.rs:89-90).  Different
+ * handles may be used concurrently, e.g. one per GPU.
+ *
+ * Errors: the reference's signatures are infallible and panic on bad sizes
+ * (fastcdc's size assert!s).  Here every call returns CDC_OK / a count >= 0,
+ * or a negative CDC_E* code, with a message from cdc_last_error().
+ */
+#ifndef CHUNKFS_AMD_H
+#define CHUNKFS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CHUNKFS_AMD_ABI_VERSION 1
+
+/* Chunk{offset,length} -- reference src/lib.rs:43-47 (usize fields; u64 here). */
+typedef struct cdc_chunk {
+    uint64_t offset;
+    uint64_t length;
+} cdc_chunk_t;
+
+/* Algorithms of reference src/chunkers/mod.rs:3-9. */
+typedef enum cdc_algo {
+    CDC_ALGO_FASTCDC = 0, /* FastChunker  (src/chunkers/fast.rs)        */
+    CDC_ALGO_FIXED = 1,   /* FSChunker    (src/chunkers/fixed_size.rs)  */
+    CDC_ALGO_RABIN = 2,   /* RabinChunker -- CDC_ENOTSUP (no oracle: cdc-chunkers 0.1.3 absent) */
+    CDC_ALGO_SUPER = 3,   /* SuperChunker -- CDC_ENOTSUP */
+    CDC_ALGO_ULTRA = 4,   /* UltraChunker -- CDC_ENOTSUP */
+    CDC_ALGO_LEAP = 5,    /* LeapChunker  -- CDC_ENOTSUP */
+    CDC_ALGO_SEQ = 6      /* SeqChunker   -- CDC_ENOTSUP */
+} cdc_algo_t;
+
+#define CDC_OK 0
+#define CDC_EINVAL (-1)  /* bad sizes / arguments (reference: fastcdc assert! panic) */
+#define CDC_ENOMEM (-2)  /* device or host allocation failed */
+#define CDC_EDEVICE (-3) /* HIP runtime error, or no usable gfx950 device */
+#define CDC_ENOTSUP (-4) /* algorithm not implemented */
+
+typedef struct cdc_handle cdc_handle_t;
+
+/* Create a chunker bound to one GPU.
+ *   CDC_ALGO_FASTCDC: FastChunker::new(SizeParams{min,avg,max}) (fast.rs:11-15);
+ *                     v2020 FastCDC, Level1 normalization (fast.rs:37).
+ *   CDC_ALGO_FIXED:   FSChunker::new(min) (fixed_size.rs:19-23); avg/max ignored.
+ * Returns CDC_OK and *out, or a negative code. */
+int cdc_create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
+               int device, cdc_handle_t **out);
+
+/* Drop(Chunker). */
+void cdc_destroy(cdc_handle_t *h);
+
+/* Chunker::chunk_data(&mut self, data: &[u8], empty: Vec<Chunk>) -> Vec<Chunk>
+ * (src/lib.rs:80).  `data` is HOST memory (borrowed for the call, any alignment,
+ * len may be 0).  Writes min(count, cap) chunks to `out` and returns the full
+ * chunk count (snprintf convention: a return > cap means `out` was too small;
+ * cdc_max_chunk_count() is always enough), or a negative CDC_E* code.
+ * The chunks tile [0, len) exactly, in order. */
+int64_t cdc_chunk_data(cdc_handle_t *h, const uint8_t *data, size_t len,
+                       cdc_chunk_t *out, size_t cap);
+
+/* Chunker::estimate_chunk_count (src/lib.rs:85): the reference's own formula,
+ * len/min for FastCDC (fast.rs:47-49), len/size + 1 for fixed
+ * (fixed_size.rs:45-47). */
+size_t cdc_estimate_chunk_count(const cdc_handle_t *h, size_t len);
+
+/* A strict upper bound on the chunk count of `len` bytes (len/min + 1). */
+size_t cdc_max_chunk_count(const cdc_handle_t *h, size_t len);
+
+/* impl Debug for the chunker (fast.rs:52-56, fixed_size.rs:12-16), with the
+ * engine suffix, e.g. "FastCDC (2020), sizes: SizeParams { min: 4096, avg:
+ * 8192, max: 16384 } [MI355X gfx950]".  Owned by the handle. */
+const char *cdc_describe(const cdc_handle_t *h);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char *cdc_last_error(void);
+
+/* Install a 256-entry GEAR table (fastcdc v2020 `GEAR`) for FastCDC handles.
+ * The built-in table is a placeholder (include/chunkfs_amd_tables.h); a
+ * maintainer pins parity with the Rust crate by passing the crate's table. */
+int cdc_set_gear(cdc_handle_t *h, const uint64_t gear[256]);
+
+/* ---- Device-resident batch API (configs 2, 4, 5: inputs already in HBM) --
+ * Chunk n independent streams in one pass.  d_streams[i] are DEVICE pointers
+ * (16-byte aligned), lens[i] their byte lengths (host arrays of n entries).
+ * The chunks of all streams are written to the DEVICE array d_out (offsets
+ * relative to each stream's start), stream i occupying
+ * d_out[first[i] .. first[i+1]); `first` is a HOST array of n+1 entries filled
+ * by the call.  out_cap must be >= cdc_batch_max_chunks().  hip_stream is a
+ * hipStream_t (NULL = the handle's own stream); the call returns after the
+ * chunks are final (it synchronises that stream).  Returns the total chunk
+ * count or a negative code.  No collective: multi-GPU runs give each rank its
+ * own handle and its own streams (weak scaling). */
+int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
+                               const uint8_t *const *d_streams,
+                               const uint64_t *lens, cdc_chunk_t *d_out,
+                               size_t out_cap, uint64_t *first,
+                               void *hip_stream);
+
+size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n,
+                            const uint64_t *lens);
+
+/* Per-phase device time of the last batch (HIP events on the launch
+ * stream), milliseconds.  scan = the gear candidate scan kernel (the HBM-bound
+ * kernel the roofline is quoted on); resolve = speculative walk + fix-up
+ * iterations; compact = scan/write of the output; total = all of it. */
+typedef struct cdc_timing {
+    double scan_ms;
+    double resolve_ms;
+    double compact_ms;
+    double total_ms;
+    uint32_t fixup_iterations;
+    uint32_t overflow_spans; /* spans whose candidate list overflowed */
+    uint64_t candidates;     /* candidate positions emitted by the scan */
+    uint64_t bytes;          /* input bytes of the batch */
+} cdc_timing_t;
+
+int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t);
+
+/* ---- Write path mirror --------------------------------
+ * ChunkStorage::write (storage.rs:78-103) + StorageWriter::{write,flush}
+ * (storage.rs:302-383) for ONE write call: 1 MiB (seg_size) slices, carry-over
+ * of the last chunk of every segment, flush of the rest.  Writes the span
+ * lengths in file order (min(count, cap) of them) and returns the span count.
+ * *chunk_seconds (may be NULL) receives the summed wall time of the
+ * chunk_data calls only, as the reference times it (storage.rs:314-316). */
+int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
+                     size_t seg_size, uint64_t *span_lengths, size_t cap,
+                     double *chunk_seconds);
+
+/* ---- Synthetic data -----------------------------------------
+ * Fill a DEVICE buffer with the splitmix64 stream: little-endian u64 words,
+ * word i = mix64(seed + (i+1) * 0x9E3779B97F4A7C15). */
+int cdc_fill_splitmix64_device(uint8_t *d_buf, size_t len, uint64_t seed,
+                               void *hip_stream);
+
+/* Engine build info, e.g. "chunkfs_amd 0.1 gfx950 abi 1". */
+const char *cdc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CHUNKFS_AMD_H */

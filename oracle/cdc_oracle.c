@@ -1,0 +1,239 @@
+/*
+ * cdc_oracle.c -- CPU ORACLE for the chunkfs chunking hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (chunkfs_amd/, include/)
+ * links, loads or calls this file.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's `cpu_baseline` leg may use it, and only as the checker / the
+ * reported CPU baseline -- never as the thing measured or shipped.
+ *
+ * It is a scalar C restatement of the algorithms behind chunkfs's
+ * `Chunker::chunk_data` (src/lib.rs:80):
+ *
+ *   - FastChunker (src/chunkers/fast.rs:29-45) -> fastcdc 3.1.0
+ *     `v2020::FastCDC::new(data, min, avg, max)` (Cargo.lock:473-476), i.e.
+ *     Normalization::Level1 and the crate's default (unseeded) GEAR table.  The
+ *     crate is NOT present in this environment; the algorithm below follows
+ *     SURVEY.md Appendix A.1-A.2 (the published fastcdc-rs v2020 `cut_gear`).
+ *   - FSChunker (src/chunkers/fixed_size.rs:32-47) -- exact, in-tree.
+ *   - StorageWriter 1 MiB segmentation with carry-over of the last chunk
+ *     (src/system/storage.rs:78-103, 302-383).
+ *
+ * PARITY STATUS
+ *   FastCDC : "parity unpinned" vs the Rust crate.  The GEAR table in
+ *             include/chunkfs_amd_tables.h is a placeholder (see that header);
+ *             the reference ships no golden vector for any CDC algorithm
+ *             (SURVEY.md §4, §8c).  This oracle is self-consistent only.
+ *   FSChunker / segmentation : pinned by the reference's own known answers
+ *             (tests/filesystem.rs:135-166, storage.rs:471-485), checked in
+ *             tests/test_oracle.py.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include <stdlib.h>
+#include <math.h>
+#include <time.h>
+
+#include "../include/chunkfs_amd_tables.h"
+
+/* fastcdc 3.1.0 v2020 size limits (assert!s in FastCDC::with_level_and_seed;
+ * SURVEY.md A.1, VERIFY).  The crate panics; the oracle returns -1. */
+#define ORC_MINIMUM_MIN 64u
+#define ORC_MINIMUM_MAX 1048576u
+#define ORC_AVERAGE_MIN 256u
+#define ORC_AVERAGE_MAX 4194304u
+#define ORC_MAXIMUM_MIN 1024u
+#define ORC_MAXIMUM_MAX 16777216u
+
+/* Level1 normalization: bits = round(log2(avg)); mask_s = MASKS[bits+1],
+ * mask_l = MASKS[bits-1]  (SURVEY.md A.1). */
+int oracle_fastcdc_masks(uint32_t min, uint32_t avg, uint32_t max,
+                         uint64_t *mask_s, uint64_t *mask_l)
+{
+    if (min < ORC_MINIMUM_MIN || min > ORC_MINIMUM_MAX) return -1;
+    if (avg < ORC_AVERAGE_MIN || avg > ORC_AVERAGE_MAX) return -1;
+    if (max < ORC_MAXIMUM_MIN || max > ORC_MAXIMUM_MAX) return -1;
+    unsigned bits = (unsigned)lround(log2((double)avg));
+    *mask_s = CHUNKFS_AMD_MASKS[bits + 1];
+    *mask_l = CHUNKFS_AMD_MASKS[bits - 1];
+    return 0;
+}
+
+/* cut_gear: returns the length of the chunk that starts at
+ * src[0], given n bytes available.  Two-bytes-per-iteration form with the
+ * pre-shifted GEAR_LS table and mask<<1 on the even byte, exactly as the
+ * crate does (odd final byte never examined; centre rounded down to even). */
+static uint64_t cut_gear(const uint8_t *src, uint64_t n, uint32_t min,
+                         uint32_t avg, uint32_t max, uint64_t mask_s,
+                         uint64_t mask_l, const uint64_t *gear,
+                         const uint64_t *gear_ls)
+{
+    uint64_t remaining = n;
+    if (remaining <= min) return remaining;
+    uint64_t center = avg;
+    if (remaining > max) remaining = max;
+    else if (remaining < center) center = remaining;
+    const uint64_t mask_s_ls = mask_s << 1, mask_l_ls = mask_l << 1;
+    uint64_t index = min / 2;
+    uint64_t hash = 0;
+    while (index < center / 2) {
+        uint64_t a = index * 2;
+        hash = (hash << 2) + gear_ls[src[a]];
+        if ((hash & mask_s_ls) == 0) return a;
+        hash = hash + gear[src[a + 1]];
+        if ((hash & mask_s) == 0) return a + 1;
+        index++;
+    }
+    while (index < remaining / 2) {
+        uint64_t a = index * 2;
+        hash = (hash << 2) + gear_ls[src[a]];
+        if ((hash & mask_l_ls) == 0) return a;
+        hash = hash + gear[src[a + 1]];
+        if ((hash & mask_l) == 0) return a + 1;
+        index++;
+    }
+    return remaining;
+}
+
+/* FastCDC v2020 iterator (offset = processed; length = cut; stop when
+ * remaining == 0), mapped to chunkfs Chunk{offset,length} (fast.rs:40-42).
+ * gear == NULL selects include/chunkfs_amd_tables.h's table.
+ * Returns the chunk count (which may exceed cap: only cap are written),
+ * or -1 on invalid sizes. */
+int64_t oracle_fastcdc_chunk(const uint8_t *data, uint64_t len, uint32_t min,
+                             uint32_t avg, uint32_t max, const uint64_t *gear,
+                             uint64_t *offsets, uint64_t *lengths, uint64_t cap)
+{
+    uint64_t ms, ml;
+    if (oracle_fastcdc_masks(min, avg, max, &ms, &ml)) return -1;
+    if (!gear) gear = CHUNKFS_AMD_GEAR;
+    uint64_t gear_ls[256];
+    for (int i = 0; i < 256; i++) gear_ls[i] = gear[i] << 1;
+    uint64_t processed = 0, count = 0;
+    while (processed < len) {
+        uint64_t cut = cut_gear(data + processed, len - processed, min, avg,
+                                max, ms, ml, gear, gear_ls);
+        if (cut == 0) break;
+        if (count < cap) {
+            if (offsets) offsets[count] = processed;
+            if (lengths) lengths[count] = cut;
+        }
+        count++;
+        processed += cut;
+    }
+    return (int64_t)count;
+}
+
+/* FSChunker::chunk_data (fixed_size.rs:32-43). */
+int64_t oracle_fixed_chunk(uint64_t len, uint64_t chunk_size,
+                           uint64_t *offsets, uint64_t *lengths, uint64_t cap)
+{
+    if (chunk_size == 0) return -1;
+    uint64_t count = 0;
+    for (uint64_t off = 0; off < len; off += chunk_size) {
+        if (count < cap) {
+            if (offsets) offsets[count] = off;
+            if (lengths) lengths[count] = (len - off < chunk_size) ? len - off : chunk_size;
+        }
+        count++;
+    }
+    return (int64_t)count;
+}
+
+/* Estimate functions: FastChunker len/min (fast.rs:47-49); FSChunker
+ * len/cs + 1 (fixed_size.rs:45-47). */
+uint64_t oracle_estimate_fast(uint64_t len, uint32_t min) { return len / min; }
+uint64_t oracle_estimate_fixed(uint64_t len, uint64_t cs) { return len / cs + 1; }
+
+/* ChunkStorage::write + StorageWriter::{write,flush} (storage.rs:78-103,
+ * 302-383) for one write call: the data is cut into seg_size slices; each
+ * slice is appended to the carried-over `rest`, chunked, the last chunk is
+ * carried again, the others become spans; flush emits the rest as one span.
+ * algo 0 = FastCDC(min,avg,max), 1 = fixed(min).  Writes span lengths (up to
+ * cap), returns the span count or -1.  *chunk_seconds accumulates the time
+ * spent inside the chunk_data calls only (storage.rs:314-316). */
+int64_t oracle_fs_write(int algo, const uint8_t *data, uint64_t len,
+                        uint32_t min, uint32_t avg, uint32_t max,
+                        const uint64_t *gear, uint64_t seg_size,
+                        uint64_t *span_lengths, uint64_t cap,
+                        double *chunk_seconds)
+{
+    if (seg_size == 0) return -1;
+    if (algo == 0) {
+        uint64_t ms, ml;
+        if (oracle_fastcdc_masks(min, avg, max, &ms, &ml)) return -1;
+    }
+    /* buffer = rest ++ slice; rest <= max (FastCDC) or <= min (fixed) */
+    uint64_t buf_cap = seg_size + (uint64_t)(max > min ? max : min) + 1;
+    uint8_t *buf = (uint8_t *)malloc(buf_cap);
+    uint64_t tmp_sz = buf_cap / (min >= 2 ? 2 * (min / 2) : 1) + 2;
+    uint64_t *tmp_len = (uint64_t *)malloc(tmp_sz * sizeof(uint64_t));
+    if (!buf || !tmp_len) { free(buf); free(tmp_len); return -1; }
+    uint64_t rest = 0, nspans = 0;
+    for (uint64_t cur = 0; cur < len;) {
+        uint64_t take = len - cur < seg_size ? len - cur : seg_size;
+        memcpy(buf + rest, data + cur, take);
+        uint64_t blen = rest + take;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        int64_t n = algo == 0
+            ? oracle_fastcdc_chunk(buf, blen, min, avg, max, gear, NULL, tmp_len, tmp_sz)
+            : oracle_fixed_chunk(blen, min, NULL, tmp_len, tmp_sz);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (chunk_seconds)
+            *chunk_seconds += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        if (n < 0) { free(buf); free(tmp_len); return -1; }
+        cur += take;
+        if (n == 0) { rest = blen; continue; } /* storage.rs:318-320 (unreachable for non-empty) */
+        uint64_t consumed = 0;
+        for (int64_t i = 0; i < n - 1; i++) {
+            if (nspans < cap && span_lengths) span_lengths[nspans] = tmp_len[i];
+            nspans++;
+            consumed += tmp_len[i];
+        }
+        rest = tmp_len[n - 1];
+        memmove(buf, buf + consumed, rest);
+    }
+    if (rest > 0) {
+        if (nspans < cap && span_lengths) span_lengths[nspans] = rest;
+        nspans++;
+    }
+    free(buf);
+    free(tmp_len);
+    return (int64_t)nspans;
+}
+
+/* Synthetic input used by every config: little-endian u64
+ * words, word i = mix64(seed + (i+1) * golden) (counter-based splitmix64). */
+static inline uint64_t mix64(uint64_t z)
+{
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+void oracle_fill_splitmix64(uint8_t *buf, uint64_t len, uint64_t seed)
+{
+    uint64_t nw = len / 8;
+    for (uint64_t i = 0; i < nw; i++) {
+        uint64_t w = mix64(seed + (i + 1) * 0x9E3779B97F4A7C15ULL);
+        memcpy(buf + 8 * i, &w, 8);
+    }
+    if (len % 8) {
+        uint64_t w = mix64(seed + (nw + 1) * 0x9E3779B97F4A7C15ULL);
+        memcpy(buf + 8 * nw, &w, len % 8);
+    }
+}
+
+/* CPU-baseline helper: wall seconds of one whole-buffer FastCDC pass
+ * (reference "raw chunk_data" mode, single thread). */
+double oracle_time_fastcdc(const uint8_t *data, uint64_t len, uint32_t min,
+                           uint32_t avg, uint32_t max, int64_t *count_out)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int64_t n = oracle_fastcdc_chunk(data, len, min, avg, max, NULL, NULL, NULL, 0);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (count_out) *count_out = n;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,173 @@
+"""ctypes wrapper of the CPU oracle (oracle/libcdc_oracle.so) + a pure-Python twin.
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product (chunkfs_amd/).
+
+Parity status: FastCDC "parity unpinned" vs the fastcdc 3.1.0 crate (the GEAR
+table is a placeholder, see include/chunkfs_amd_tables.h); FSChunker and the
+1 MiB write-path segmentation are pinned by the reference's known answers
+(tests/filesystem.rs:135-166, src/system/storage.rs:471-485).
+"""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libcdc_oracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.oracle_fastcdc_chunk.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                           u64p, u64p, ctypes.c_uint64]
+        L.oracle_fastcdc_chunk.restype = ctypes.c_int64
+        L.oracle_fixed_chunk.argtypes = [ctypes.c_uint64, ctypes.c_uint64, u64p, u64p, ctypes.c_uint64]
+        L.oracle_fixed_chunk.restype = ctypes.c_int64
+        L.oracle_fs_write.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
+                                      u64p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_fs_write.restype = ctypes.c_int64
+        L.oracle_fill_splitmix64.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_fill_splitmix64.restype = None
+        L.oracle_fastcdc_masks.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u64p, u64p]
+        L.oracle_fastcdc_masks.restype = ctypes.c_int
+        L.oracle_time_fastcdc.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int64)]
+        L.oracle_time_fastcdc.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u64p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def splitmix64_bytes(n, seed):
+    buf = np.empty(n, dtype=np.uint8)
+    lib().oracle_fill_splitmix64(_ptr(buf), n, seed)
+    return buf
+
+
+def masks(mn, avg, mx):
+    s, l = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().oracle_fastcdc_masks(mn, avg, mx, ctypes.byref(s), ctypes.byref(l))
+    if rc:
+        raise ValueError("invalid FastCDC sizes")
+    return s.value, l.value
+
+
+def fastcdc(data, mn, avg, mx, gear=None):
+    """(n, 2) uint64 array of (offset, length): FastCDC v2020 over the whole buffer."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    n = data.size
+    cap = n // max(2 * (mn // 2), 1) + 2
+    off = np.empty(cap, dtype=np.uint64)
+    ln = np.empty(cap, dtype=np.uint64)
+    g = None if gear is None else np.ascontiguousarray(gear, dtype=np.uint64)
+    cnt = lib().oracle_fastcdc_chunk(_ptr(data), n, mn, avg, mx, None if g is None else _ptr(g),
+                                     _u64p(off), _u64p(ln), cap)
+    if cnt < 0:
+        raise ValueError("invalid FastCDC sizes")
+    assert cnt <= cap
+    return np.stack([off[:cnt], ln[:cnt]], axis=1)
+
+
+def fixed(n, cs):
+    cap = n // cs + 2
+    off = np.empty(cap, dtype=np.uint64)
+    ln = np.empty(cap, dtype=np.uint64)
+    cnt = lib().oracle_fixed_chunk(n, cs, _u64p(off), _u64p(ln), cap)
+    return np.stack([off[:cnt], ln[:cnt]], axis=1)
+
+
+def fs_write(algo, data, mn, avg=0, mx=0, seg_size=1 << 20, gear=None):
+    """StorageWriter mirror: span lengths of one write call, and summed chunk_data seconds."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    cap = data.size // max(2 * (mn // 2), 1) + 2
+    out = np.empty(cap, dtype=np.uint64)
+    secs = ctypes.c_double(0.0)
+    g = None if gear is None else np.ascontiguousarray(gear, dtype=np.uint64)
+    cnt = lib().oracle_fs_write(0 if algo == "fast" else 1, _ptr(data), data.size, mn, avg, mx,
+                                None if g is None else _ptr(g), seg_size, _u64p(out), cap,
+                                ctypes.byref(secs))
+    if cnt < 0:
+        raise ValueError("invalid arguments")
+    return out[:cnt], secs.value
+
+
+def time_fastcdc(data, mn, avg, mx):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    c = ctypes.c_int64()
+    t = lib().oracle_time_fastcdc(_ptr(data), data.size, mn, avg, mx, ctypes.byref(c))
+    return t, c.value
+
+
+# ---------------------------------------------------------------------------
+# Pure-Python twin (small inputs only): an independent restatement of
+# SURVEY.md Appendix A.2 in the BYTE-WISE form  h = (h << 1) + GEAR[b],
+# tested against the mask at every position -- a different code shape from the
+# C oracle's two-bytes-per-iteration loop, so the two cross-check each other.
+
+def _tables():
+    path = os.path.join(ROOT, "include", "chunkfs_amd_tables.h")
+    txt = open(path).read()
+    import re
+    def grab(name):
+        body = txt.split(name, 1)[1].split("{", 1)[1].split("}", 1)[0]
+        return [int(x, 16) for x in re.findall(r"0x([0-9A-Fa-f]+)ULL", body)]
+    return grab("CHUNKFS_AMD_GEAR["), grab("CHUNKFS_AMD_MASKS[")
+
+
+def py_fastcdc(data, mn, avg, mx, gear=None):
+    g, M = _tables()
+    if gear is not None:
+        g = [int(x) for x in gear]
+    bits = int(round(math.log2(avg)))
+    ms, ml = M[bits + 1], M[bits - 1]
+    data = bytes(bytearray(np.asarray(data, dtype=np.uint8)))
+    out = []
+    pos = 0
+    n = len(data)
+    M64 = (1 << 64) - 1
+    while pos < n:
+        rem = n - pos
+        if rem <= mn:
+            cut = rem
+        else:
+            center = avg
+            if rem > mx:
+                rem = mx
+            elif rem < center:
+                center = rem
+            a0, ce, re_ = (mn // 2) * 2, (center // 2) * 2, (rem // 2) * 2
+            h = 0
+            cut = rem
+            for p in range(a0, re_):
+                h = ((h << 1) + g[data[pos + p]]) & M64
+                if h & (ms if p < ce else ml) == 0:
+                    cut = p
+                    break
+        out.append((pos, cut))
+        pos += cut
+    return np.array(out, dtype=np.uint64).reshape(-1, 2)

@@ -1,0 +1,219 @@
+"""GPU parity suite (-m gpu): the HIP engine through the C ABI vs the CPU oracle.
+
+Bit-exact (integer / index work): every (offset, length) must equal the
+oracle's on the same bytes.  FastCDC parity is vs the oracle restatement
+(parity vs the fastcdc 3.1.0 crate is unpinned: GEAR placeholder); FSChunker
+and the write path are additionally pinned by the reference's known answers.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from gen_golden import make_input
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+SIZES = [(4096, 8192, 16384), (8192, 16384, 65536), (2048, 8192, 65536), (512, 2048, 16384),
+         (16384, 65536, 262144), (64, 256, 1024), (8192, 4096, 16384)]
+
+_cache = {}
+
+
+def chunker(sizes):
+    import chunkfs_amd as c
+    if sizes not in _cache:
+        _cache[sizes] = c.FastChunker(c.SizeParams(*sizes))
+    return _cache[sizes]
+
+
+def assert_same(gpu, ref, what=""):
+    gpu = np.asarray(gpu, dtype=np.uint64).reshape(-1, 2)
+    ref = np.asarray(ref, dtype=np.uint64).reshape(-1, 2)
+    if gpu.shape != ref.shape or not (gpu == ref).all():
+        n = min(len(gpu), len(ref))
+        bad = np.nonzero((gpu[:n] != ref[:n]).any(axis=1))[0]
+        i = int(bad[0]) if len(bad) else n
+        pytest.fail(f"{what}: {len(gpu)} vs {len(ref)} chunks; first mismatch at #{i}: "
+                    f"gpu={gpu[i].tolist() if i < len(gpu) else None} ref={ref[i].tolist() if i < len(ref) else None}")
+
+
+def test_golden_vectors_on_gpu():
+    with open(os.path.join(GOLDEN, "fastcdc_selfconsistent.json")) as f:
+        vecs = json.load(f)["vectors"]
+    for v in vecs:
+        data = make_input(v["pattern"], v["len"], v["seed"])
+        assert hashlib.sha256(data.tobytes()).hexdigest() == v["input_sha256"]
+        got = chunker((v["min"], v["avg"], v["max"])).chunk_array(data)
+        assert [int(x) for x in got[:, 1]] == v["lengths"], (v["pattern"], v["len"], v["min"])
+
+
+@pytest.mark.parametrize("sizes", SIZES)
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_streams_bit_exact(sizes, seed):
+    for n in [3 * (1 << 20) + 17 * seed, (1 << 20)]:
+        data = oracle.splitmix64_bytes(n, seed * 31 + n)
+        assert_same(chunker(sizes).chunk_array(data), oracle.fastcdc(data, *sizes), f"{sizes} n={n}")
+
+
+def test_tails_of_every_length():
+    """Every length 0 .. 2*max+1 around the min/max thresholds (CS-3 edge cases)."""
+    sizes = (4096, 8192, 16384)
+    base = oracle.splitmix64_bytes(2 * 16384 + 64, 77)
+    c = chunker(sizes)
+    lens = list(range(0, 200)) + list(range(4000, 4200)) + list(range(8100, 8300)) + \
+        list(range(16300, 16500)) + list(range(2 * 16384 - 100, 2 * 16384 + 2))
+    for n in lens:
+        assert_same(c.chunk_array(base[:n]), oracle.fastcdc(base[:n], *sizes), f"n={n}")
+
+
+@pytest.mark.parametrize("pattern,n,seed", [
+    ("const", 5 << 20, 0), ("const", 3 << 20, 0xFF), ("const", 3 << 20, 0x5A),
+    ("periodic", 4 << 20, 61), ("periodic", 4 << 20, 4096), ("periodic", 4 << 20, 1),
+    ("lowentropy", 4 << 20, 11), ("lowentropy", 4 << 20, 12)])
+def test_low_entropy_and_overflow_paths(pattern, n, seed):
+    """Constant / periodic data: candidate lists are empty or overflow (slow exact path)."""
+    data = make_input(pattern, n, seed)
+    for sizes in [(4096, 8192, 16384), (512, 2048, 16384)]:
+        assert_same(chunker(sizes).chunk_array(data), oracle.fastcdc(data, *sizes), f"{pattern} {sizes}")
+
+
+def test_unaligned_host_buffer():
+    data = oracle.splitmix64_bytes((1 << 20) + 100, 5)
+    for shift in [1, 3, 7, 13]:
+        view = data[shift:]
+        assert_same(chunker(SIZES[0]).chunk_array(view), oracle.fastcdc(view, *SIZES[0]), f"shift={shift}")
+
+
+def test_chunk_data_mirror_and_estimate():
+    import chunkfs_amd as c
+    ch = chunker(SIZES[0])
+    data = oracle.splitmix64_bytes(100_000, 3)
+    got = ch.chunk_data(data.tobytes())
+    ref = oracle.fastcdc(data, *SIZES[0])
+    assert [(x.offset(), x.length()) for x in got] == [tuple(map(int, r)) for r in ref]
+    assert ch.estimate_chunk_count(data) == 100_000 // 4096       # fast.rs:47-49
+    assert ch.chunk_data(b"") == []
+    assert "FastCDC (2020), sizes: SizeParams { min: 4096, avg: 8192, max: 16384 }" in repr(ch)
+    fs = c.FSChunker(4096)
+    assert fs.estimate_chunk_count(data) == 100_000 // 4096 + 1   # fixed_size.rs:45-47
+
+
+@pytest.mark.parametrize("cs", [1, 7, 4096, 8192, 65536])
+def test_fixed_size_chunker(cs):
+    import chunkfs_amd as c
+    fs = c.FSChunker(cs)
+    for n in [0, 1, cs - 1 if cs > 1 else 2, cs, cs + 1, 3 * (1 << 20) + 50]:
+        data = np.zeros(n, dtype=np.uint8)
+        assert_same(fs.chunk_array(data), oracle.fixed(n, cs), f"cs={cs} n={n}")
+
+
+def test_write_path_fixed_known_answers():
+    """tests/filesystem.rs:135-166: FSChunker(4096) dedup ratios 256, 512, 384 through the GPU write path."""
+    import chunkfs_amd as c
+    fs = c.FSChunker(4096)
+    db, written, ratios = {}, 0, []
+    for val in [10, 10, 20]:
+        data = np.full(1 << 20, val, dtype=np.uint8)
+        spans, _ = c.write_spans(fs, data)
+        off = 0
+        for ln in spans:
+            db.setdefault(hashlib.sha256(data[off:off + int(ln)].tobytes()).digest(), int(ln))
+            off += int(ln)
+        assert off == len(data)
+        written += len(data)
+        ratios.append(written / sum(db.values()))
+    assert ratios == pytest.approx([256.0, 512.0, 384.0])
+
+
+@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (8192, 16384, 65536)])
+def test_write_path_segmentation_invariance(sizes):
+    """spans via the 1 MiB write path == one chunk_data over the whole write == oracle."""
+    import chunkfs_amd as c
+    data = oracle.splitmix64_bytes(5 * (1 << 20) + 4321, 9)
+    spans, secs = c.write_spans(chunker(sizes), data)
+    ref_spans, _ = oracle.fs_write("fast", data, *sizes)
+    whole = oracle.fastcdc(data, *sizes)[:, 1]
+    assert spans.tolist() == ref_spans.tolist() == whole.tolist()
+    assert secs > 0
+
+
+def _torch_batch(ch, arrays):
+    import torch
+    dev = torch.device("cuda", 0)
+    bufs = [torch.from_numpy(a).to(dev) if len(a) else torch.empty(16, dtype=torch.uint8, device=dev)
+            for a in arrays]
+    lens = [len(a) for a in arrays]
+    cap = ch.batch_max_chunks(lens)
+    out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=dev)
+    first = ch.chunk_batch_device([b.data_ptr() for b in bufs], lens, out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint64), first
+
+
+def test_ragged_batch_device():
+    sizes = SIZES[0]
+    ch = chunker(sizes)
+    lens = [0, 1, 4096, 65536, 65537, 3 << 20, 100, 0, (1 << 20) + 12345, 16385, 2 * 65536]
+    arrays = [oracle.splitmix64_bytes(n, 1000 + i) for i, n in enumerate(lens)]
+    out, first = _torch_batch(ch, arrays)
+    assert first[0] == 0
+    for i, a in enumerate(arrays):
+        assert_same(out[first[i]:first[i + 1]], oracle.fastcdc(a, *sizes), f"stream {i} len={len(a)}")
+
+
+def test_batch_composition_invariance():
+    """Determinism: a stream's chunks do not depend on what else is in the batch."""
+    sizes = SIZES[0]
+    ch = chunker(sizes)
+    a = oracle.splitmix64_bytes(2 << 20, 5)
+    alone, f1 = _torch_batch(ch, [a])
+    mixed, f2 = _torch_batch(ch, [oracle.splitmix64_bytes(777777, 6), a, oracle.splitmix64_bytes(12345, 7)])
+    assert (alone[f1[0]:f1[1]] == mixed[f2[1]:f2[2]]).all()
+
+
+def test_custom_gear_table():
+    sizes = SIZES[0]
+    import chunkfs_amd as c
+    ch = c.FastChunker(c.SizeParams(*sizes))
+    gear = oracle.splitmix64_bytes(256 * 8, 12345).view(np.uint64).copy()
+    ch.set_gear(gear)
+    data = oracle.splitmix64_bytes(2 << 20, 8)
+    assert_same(ch.chunk_array(data), oracle.fastcdc(data, *sizes, gear=gear), "custom gear")
+
+
+def test_device_generator_matches_oracle():
+    import ctypes
+    import torch
+    from chunkfs_amd import _lib
+    n = (1 << 20) + 13
+    buf = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(buf.data_ptr()), n, 1, None))
+    assert (buf[:n].cpu().numpy() == oracle.splitmix64_bytes(n, 1)).all()
+
+
+def test_one_gib_stream_and_timing():
+    """Config 2 at full size: 1 GiB splitmix64(seed=1), FastCDC 4/8/16, bit-exact."""
+    import ctypes
+    import torch
+    from chunkfs_amd import _lib
+    sizes = SIZES[0]
+    ch = chunker(sizes)
+    n = 1 << 30
+    buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(buf.data_ptr()), n, 1, None))
+    cap = ch.batch_max_chunks([n])
+    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda")
+    first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+    got = out[:int(first[1])].cpu().numpy().view(np.uint64)
+    ref = oracle.fastcdc(buf.cpu().numpy(), *sizes)
+    assert_same(got, ref, "1 GiB")
+    t = ch.last_timing()
+    assert t["bytes"] == n and t["scan_ms"] > 0 and t["overflow_spans"] == 0
+    # size-independent properties
+    assert int(got[:, 1].sum()) == n
+    assert (got[:-1, 1] >= sizes[0]).all() and (got[:, 1] <= sizes[2]).all()
