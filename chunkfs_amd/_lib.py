@@ -4,6 +4,7 @@ Loading fails loudly: there is no CPU fallback anywhere in the product.
 """
 import ctypes
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libchunkfs_amd.so")
@@ -60,6 +61,17 @@ def lib():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the HIP engine is the only implementation; there is no CPU fallback)")
+    # PyTorch-ROCm wheels bundle their own libamdhip64 (same SONAME
+    # libamdhip64.so.7 as /opt/rocm's).  If ours were loaded first, a later
+    # `import torch` would map a SECOND HIP runtime into the process and fail
+    # ("No HIP GPUs are available").  Importing torch first makes our NEEDED
+    # libamdhip64.so.7 resolve to the already-loaded copy: one runtime, shared
+    # device pointers and streams.  Without torch the system runtime is used.
+    if "torch" not in sys.modules and not os.environ.get("CHUNKFS_AMD_NO_TORCH"):
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.c_void_p
     u8p = ctypes.POINTER(ctypes.c_uint8)

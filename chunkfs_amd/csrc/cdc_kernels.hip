@@ -30,11 +30,28 @@
 namespace cdc {
 namespace {
 
-constexpr int kScanThreads = 512;
+constexpr int kScanThreads = 1024;
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kCopies = 32;           // GEAR replicas, one bank pair per lane&31
-constexpr uint32_t kIterBytes = 1024; // 64 lanes x 16 B per wave-iteration
-constexpr int kPrefetch = 4;          // wave-iterations of loads kept in flight
+constexpr uint32_t kIterBytes = 4096; // 64 lanes x 64 contiguous bytes per wave-iteration
+constexpr uint32_t kEntCap = 64;      // per-wave LDS list of hitting 16-byte quarters per span
+// Candidate record: offset in span (spans <= 16 MiB) | exact mask hit flags.
+constexpr uint32_t kCandPosMask = 0x00FFFFFFu;
+constexpr uint32_t kCandHitL = 1u << 30;
+constexpr uint32_t kCandHitS = 1u << 31;
+
+// Global (address space 1) views of the stream bytes.  Generic pointers would
+// compile to flat_load_*, which count on both vmcnt and lgkmcnt and may return
+// out of order: every LDS wait would then drain the whole prefetch ring.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef const __attribute__((address_space(1))) uint8_t g_u8;
+__device__ __forceinline__ g_u32x4 *as_global4(const void *p) { return (g_u32x4 *)(p); }
+__device__ __forceinline__ g_u8 *as_global1(const void *p) { return (g_u8 *)(p); }
+__device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
+    const u32x4 v = *p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // DPP wave_shr:1 (dpp_ctrl 0x138): lane i receives lane i-1; lane 0 keeps `fill`.
 __device__ __forceinline__ uint64_t wave_shr1(uint64_t v, uint64_t fill) {
@@ -72,24 +89,85 @@ __device__ __forceinline__ uint32_t cand_test(uint64_t h, const FastParams &fp) 
     }
 }
 
-// GEAR[b] for byte j (0..15) of the lane's 16 bytes: one v_perm_b32 builds the
-// LDS byte address b*256 + (lane&31)*8, one ds_read_b64 fetches the entry.
-__device__ __forceinline__ void gather16(const char *tabb, uint32_t lane_off,
-                                         const uint4 v, uint64_t (&gj)[16]) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t addr = __builtin_amdgcn_perm(
-            lane_off, w[j >> 2], 0x0c0c0004u | ((uint32_t)(j & 3) << 8));
-        gj[j] = *reinterpret_cast<const uint64_t *>(tabb + addr);
-    }
+// h = (h << 1) + g as ONE opaque v_lshl_add_u64.  Plain C lets LLVM
+// reassociate a 48-term chain into a tree that keeps every lookup live (2
+// VGPRs each) and spills; the asm keeps the chain strictly sequential, so each
+// GEAR lookup dies right after its add.
+__device__ __forceinline__ uint64_t shl1_add(uint64_t h, uint64_t g) {
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 1, %2" : "=v"(r) : "v"(h), "v"(g));
+    return r;
 }
 
+// GEAR[byte b of word w] from LDS: one v_perm_b32 builds the byte address
+// b*256 + replica*8, one ds_read_b64 fetches the entry.
+__device__ __forceinline__ uint64_t gear_of(const char *tabb, uint32_t rep_off, uint32_t w, int b) {
+    const uint32_t addr = __builtin_amdgcn_perm(rep_off, w, 0x0c0c0004u | ((uint32_t)b << 8));
+    return *reinterpret_cast<const uint64_t *>(tabb + addr);
+}
+
+struct Data64 {
+    uint4 q[4];
+};
+
+__device__ __forceinline__ Data64 ld64(g_u32x4 *p) {
+    Data64 d;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d.q[i] = ld16(p + i);
+    return d;
+}
+
+__device__ __forceinline__ uint32_t word_of(const uint4 &v, int w) {
+    return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
+}
+
+// Hash of the lane's 64 bytes from a zero state, mod 2^48: only the last 48
+// bytes can reach bits 0..47, so bytes 16..63 suffice.  It equals the TRUE
+// (windowed) hash at the lane's last byte.  Uses a different GEAR replica than
+// pass 2 so the compiler cannot keep these 48 lookups live for reuse.
+__device__ __forceinline__ uint64_t pass1(const char *tabb, uint32_t rep_off, const Data64 &d) {
+    uint64_t P = 0;
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) P = shl1_add(P, gear_of(tabb, rep_off, word_of(d.q[q], w), b));
+        // Bound the scheduler's lookahead to one 16-byte quarter: hoisting all
+        // lookups of the lane at once costs ~2 VGPRs each and spills.
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return P;
+}
+
+__device__ __forceinline__ uint4 ld16_guarded(const uint8_t *base, uint32_t p, uint32_t limit) {
+    if (p + 16 <= limit) return ld16(as_global4(base + p));
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (p < limit) {
+        g_u8 *gb = as_global1(base);
+        for (uint32_t j = 0; p + j < limit; ++j) w[j >> 2] |= (uint32_t)gb[p + j] << (8 * (j & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// One-pass gear candidate scan.  Layout: one wavefront per span; per
+// wave-iteration the 64 lanes cover 4 KiB, lane l owning the contiguous bytes
+// [64 l, 64 l + 64).  Per lane: pass 1 (48 lookups) gives the lane's end hash;
+// one DPP wave_shr hands it to lane l+1 as its carry-in (bits 0..47 exact: no
+// multi-step scan needed once a lane owns >= 48 bytes); pass 2 walks the 64
+// positions with the true hash and tests (h & cmask) == 0, min-accumulated per
+// 16-byte quarter.  A hitting quarter only appends (position, hash before the
+// quarter) to a per-wave LDS list; exact mask_s/mask_l flags, ordering and the
+// HBM write happen once per span in the flush.
 template <bool kAlign>
 __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
     const StreamTable st, const FastParams fp,
     const uint64_t *__restrict__ gear, const Candidates cand) {
     __shared__ uint64_t tab[256 * kCopies];  // 64 KiB: entry e, replica c at e*32+c
+    __shared__ uint32_t epos[kScanWaves][kEntCap];
+    __shared__ uint32_t ehlo[kScanWaves][kEntCap];
+    __shared__ uint32_t ehhi[kScanWaves][kEntCap];
+    __shared__ uint32_t ecnt[kScanWaves][kEntCap];
     for (int i = threadIdx.x; i < 256 * kCopies; i += kScanThreads)
         tab[i] = gear[i / kCopies];
     __syncthreads();
@@ -97,8 +175,10 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
     const char *tabb = reinterpret_cast<const char *>(tab);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t lane_off = (lane & 31) * 8;
+    const uint32_t rep2 = (lane & 31) * 8;         // pass-2 replica
+    const uint32_t rep1 = ((lane + 16) & 31) * 8;  // pass-1 replica (still a permutation)
     const uint64_t span = 1ull << st.span_log2;
+    const uint64_t lanemask_lt = (1ull << lane) - 1;
 
     for (uint64_t g = (uint64_t)blockIdx.x * kScanWaves + wave; g < st.total_spans;
          g += (uint64_t)gridDim.x * kScanWaves) {
@@ -108,212 +188,280 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
         const uint8_t *base = st.ptrs[si] + off;
         const uint64_t n_left = st.lens[si] - off;
         const uint32_t span_len = (uint32_t)(n_left < span ? n_left : span);
-        uint32_t *cpos = cand.pos + g * cand.cap;
-        uint64_t *chash = cand.hash + g * cand.cap;
 
-        // Carry-in: windowed hash of byte off-1 from the 48 bytes before the span
-        // (lanes 61..63 hold them; earlier history cannot reach bits 0..47).
+        // Carry-in: true hash of byte off-1 = pass 1 over the 64 bytes before the span.
         uint64_t carry = 0;
         if (off != 0) {
             uint64_t P = 0;
-            if (lane >= 61) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(base - 48 + (lane - 61) * 16);
-                uint64_t gj[16];
-                gather16(tabb, lane_off, v, gj);
-#pragma unroll
-                for (int j = 0; j < 16; ++j) P = (P << 1) + gj[j];
-            }
-            uint64_t E = P + (wave_shr1(P, 0) << 16);
-            E = P + (wave_shr1(E, 0) << 16);
-            E = P + (wave_shr1(E, 0) << 16);
-            carry = readlane63(E);
+            if (lane == 63) P = pass1(tabb, rep1, ld64(as_global4(base - 64)));
+            carry = readlane63(P);
         }
 
-        uint32_t wcount = 0;  // candidates emitted so far in this span (wave-uniform)
+        uint32_t ne = 0;  // quarter entries appended this span (wave-uniform)
 
-        auto process = [&](const uint4 v, uint32_t pos0, uint32_t valid) {
-            uint64_t gj[16];
-            gather16(tabb, lane_off, v, gj);
-            uint64_t P = 0;  // lane-local hash of its 16 bytes from a zero state
-#pragma unroll
-            for (int j = 0; j < 16; ++j) P = (P << 1) + gj[j];
-            // End-of-lane true hash, exact mod 2^48 after 3 steps.
-            uint64_t E = P + (wave_shr1(P, carry) << 16);
-            E = P + (wave_shr1(E, carry) << 16);
-            E = P + (wave_shr1(E, carry) << 16);
-            const uint64_t cin = wave_shr1(E, carry);
-            carry = readlane63(E);
+        auto process = [&](const Data64 d, uint32_t pos0, uint32_t qvalid) {
+            const uint64_t P = pass1(tabb, rep1, d);
+            const uint64_t cin = wave_shr1(P, carry);
+            carry = readlane63(P);
             uint64_t h = cin;
-            uint32_t acc = 0xffffffffu;
+            uint64_t hq[4];
+            uint32_t nq = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                h = (h << 1) + gj[j];
-                acc = min(acc, cand_test<kAlign>(h, fp));
-            }
-            const bool maybe = acc == 0;
-            if (__ballot(maybe)) {  // rare: ~1 lane in 256 per iteration at 12-bit masks
-                uint32_t hm = 0;
-                if (maybe) {
-                    uint64_t hh = cin;
+            for (int q = 0; q < 4; ++q) {
+                hq[q] = h;
+                uint32_t acc = 0xffffffffu;
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) {
-                        hh = (hh << 1) + gj[j];
-                        if (cand_test<kAlign>(hh, fp) == 0 && (uint32_t)j < valid) hm |= 1u << j;
+                for (int w = 0; w < 4; ++w)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        h = shl1_add(h, gear_of(tabb, rep2, word_of(d.q[q], w), b));
+                        acc = min(acc, cand_test<kAlign>(h, fp));
                     }
-                }
-                const uint32_t cnt = __popc(hm);
-                uint32_t incl = cnt;
+                nq |= (uint32_t)(acc == 0) << q;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            nq &= qvalid;
+            if (__ballot(nq != 0)) {  // ~1 hitting quarter per 4 KiB at 12-bit masks
 #pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t t = __shfl_up(incl, d);
-                    if (lane >= (uint32_t)d) incl += t;
-                }
-                const uint32_t total = __shfl(incl, 63);
-                if (hm) {
-                    uint32_t slot = wcount + incl - cnt;
-                    uint64_t hh = cin;
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) {
-                        hh = (hh << 1) + gj[j];
-                        if ((hm >> j) & 1u) {
-                            if (slot < cand.cap) {
-                                cpos[slot] = pos0 + j;
-                                chash[slot] = hh;
-                            }
-                            ++slot;
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t m = __ballot((nq >> q) & 1u);
+                    if ((nq >> q) & 1u) {
+                        const uint32_t slot = ne + (uint32_t)__popcll(m & lanemask_lt);
+                        if (slot < kEntCap) {
+                            epos[wave][slot] = pos0 + 16 * q;
+                            ehlo[wave][slot] = (uint32_t)hq[q];
+                            ehhi[wave][slot] = (uint32_t)(hq[q] >> 32);
                         }
                     }
+                    ne += (uint32_t)__popcll(m);
                 }
-                wcount += total;
             }
         };
 
         const uint32_t nfull = span_len / kIterBytes;
-        const uint4 *vb = reinterpret_cast<const uint4 *>(base) + lane;
-        uint4 pf[kPrefetch];
-#pragma unroll
-        for (int d = 0; d < kPrefetch; ++d) {
-            const uint32_t it = (uint32_t)d < nfull ? d : (nfull ? nfull - 1 : 0);
-            pf[d] = nfull ? vb[it * 64] : make_uint4(0, 0, 0, 0);
-        }
-        for (uint32_t it = 0; it < nfull; it += kPrefetch) {
-#pragma unroll
-            for (int d = 0; d < kPrefetch; ++d) {
-                if (it + d < nfull) {
-                    const uint4 v = pf[d];
-                    const uint32_t nx = min(it + d + kPrefetch, nfull - 1);
-                    pf[d] = vb[nx * 64];
-                    process(v, (it + d) * kIterBytes + lane * 16, 16);
-                }
+        g_u32x4 *vb = as_global4(base) + lane * 4;
+        uint32_t it = 0;
+        if (nfull >= 2) {
+            Data64 A = ld64(vb);
+            __builtin_amdgcn_sched_barrier(0);
+            Data64 B = ld64(vb + 256);
+            __builtin_amdgcn_sched_barrier(0);
+            for (; it + 2 <= nfull; it += 2) {
+                // Consume a buffer, then refill it two iterations ahead (same
+                // registers: no loop-carried copies of in-flight loads).
+                process(A, it * kIterBytes + lane * 64, 0xFu);
+                A = ld64(vb + min(it + 2, nfull - 1) * 256);
+                process(B, (it + 1) * kIterBytes + lane * 64, 0xFu);
+                B = ld64(vb + min(it + 3, nfull - 1) * 256);
             }
         }
+        for (; it < nfull; ++it)  // remainder: only in the last span of a stream
+            process(ld64(vb + it * 256), it * kIterBytes + lane * 64, 0xFu);
         if (span_len % kIterBytes) {  // ragged end of a stream: guarded loads
-            const uint32_t pos0 = nfull * kIterBytes + lane * 16;
-            const uint32_t valid = pos0 < span_len ? min(span_len - pos0, 16u) : 0u;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (valid == 16) {
-                v = *reinterpret_cast<const uint4 *>(base + pos0);
-            } else if (valid) {
-                uint32_t w[4] = {0, 0, 0, 0};
-                for (uint32_t j = 0; j < valid; ++j) w[j >> 2] |= (uint32_t)base[pos0 + j] << (8 * (j & 3));
-                v = make_uint4(w[0], w[1], w[2], w[3]);
+            const uint32_t pos0 = nfull * kIterBytes + lane * 64;
+            Data64 d;
+            uint32_t qvalid = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t p = pos0 + 16 * q;
+                if (p < span_len) qvalid |= 1u << q;
+                d.q[q] = ld16_guarded(base, p, span_len);
             }
-            process(v, pos0, valid);
+            process(d, pos0, qvalid);
         }
-        if (lane == 0) cand.count[g] = wcount;
+
+        // Flush: exact flags for each hitting quarter, position order, HBM write.
+        uint32_t *cpos = cand.pos + g * cand.cap;
+        if (ne > kEntCap) {  // too many hits for the LDS list: resolver takes the exact slow path
+            if (lane == 0) cand.count[g] = cand.cap + 1;
+            continue;
+        }
+        uint32_t hs = 0, hl = 0, my_pos = 0;
+        if (lane < ne) {
+            my_pos = epos[wave][lane];
+            uint64_t hh = ((uint64_t)ehhi[wave][lane] << 32) | ehlo[wave][lane];
+            const uint4 v = ld16_guarded(base, my_pos, span_len);
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int j = 4 * w + b;
+                    hh = (hh << 1) + gear_of(tabb, rep2, word_of(v, w), b);
+                    if (my_pos + j < span_len) {
+                        hs |= (uint32_t)((hh & fp.mask_s) == 0) << j;
+                        hl |= (uint32_t)((hh & fp.mask_l) == 0) << j;
+                    }
+                }
+            ecnt[wave][lane] = __popc(hs | hl);
+        }
+        // Output slot = records of all entries at lower positions (entries are
+        // few: a linear rank over the wave's LDS list).
+        uint32_t slot = 0, total = 0;
+        for (uint32_t k = 0; k < ne; ++k) {
+            const uint32_t c = ecnt[wave][k];
+            total += c;
+            if (epos[wave][k] < my_pos) slot += c;
+        }
+        if (lane < ne) {
+            for (uint32_t m = hs | hl; m; m &= m - 1) {
+                const uint32_t j = __builtin_ctz(m);
+                if (slot < cand.cap)
+                    cpos[slot] = (my_pos + j) | (((hs >> j) & 1u) << 31) | (((hl >> j) & 1u) << 30);
+                ++slot;
+            }
+        }
+        if (lane == 0) cand.count[g] = total;
     }
 }
 
 // ---------------------------------------------------------------------------
-// Resolve.  `tab` is a single LDS copy of GEAR.
+// Resolve.  One thread walks one chain; `tab` is a single LDS copy of GEAR and
+// `win` the thread's 64-byte LDS window for the truncated-hash check.
 
-// Exact sequential cut (byte-wise form of cut_gear): only used
-// when a candidate list overflowed (pathological, low-entropy data).
-__device__ uint64_t slow_cut(const FastParams &fp, const uint64_t *tab,
-                             const uint8_t *d, uint64_t n, uint64_t s) {
-    uint64_t rem = n - s;
-    if (rem <= fp.min) return n;
-    uint64_t center = fp.avg;
-    if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
-    const uint64_t a0 = (fp.min / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
-    uint64_t h = 0;
-    for (uint64_t p = a0; p < re; ++p) {
-        h = (h << 1) + tab[d[s + p]];
-        if (!(h & (p < ce ? fp.mask_s : fp.mask_l))) return s + p;
-    }
-    return s + rem;
-}
+constexpr int kResolveThreads = 256;
+constexpr uint32_t kWin = 64;
 
-// Cut point (end offset) of the chunk that starts at s, from the candidates.
-__device__ uint64_t next_cut(const StreamTable &st, const FastParams &fp,
-                             const Candidates &cand, const uint64_t *tab,
-                             const uint8_t *d, uint64_t n, uint64_t gbase,
-                             uint64_t s) {
-    uint64_t rem = n - s;
-    if (rem <= fp.min) return n;                   // tail chunk
-    uint64_t center = fp.avg;
-    if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
-    const uint64_t a0 = (fp.min / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
-    const uint64_t tl = min(a0 + (uint64_t)fp.trunc, re);
-    // Positions where the in-chunk hash (reset at s+a0) still differs from W.
-    uint64_t h = 0;
-    for (uint64_t p = a0; p < tl; ++p) {
-        h = (h << 1) + tab[d[s + p]];
-        if (!(h & (p < ce ? fp.mask_s : fp.mask_l))) return s + p;
+struct Walker {
+    const StreamTable &st;
+    const FastParams &fp;
+    const Candidates &cand;
+    const uint64_t *tab;
+    uint8_t *win;
+    const uint8_t *data;
+    uint64_t n;
+    uint64_t gbase;
+    // Monotonic candidate cursor: along one chain every window starts after
+    // the previous one, so each candidate record is read at most once.
+    uint64_t cur_sp = ~0ull;
+    uint32_t cur_k = 0;
+
+    // Exact sequential cut (byte-wise form of cut_gear); used
+    // only when a span's candidate list overflowed (low-entropy data).
+    __device__ uint64_t slow_cut(uint64_t s) {
+        g_u8 *d = as_global1(data);
+        uint64_t rem = n - s;
+        uint64_t center = fp.avg;
+        if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
+        const uint64_t a0 = (fp.min / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
+        uint64_t h = 0;
+        for (uint64_t p = a0; p < re; ++p) {
+            h = (h << 1) + tab[d[s + p]];
+            if (!(h & (p < ce ? fp.mask_s : fp.mask_l))) return s + p;
+        }
+        return s + rem;
     }
-    if (tl < re) {
-        const uint64_t lo = s + tl, hi = s + re;
-        for (uint64_t sp = lo >> st.span_log2; (sp << st.span_log2) < hi; ++sp) {
-            const uint64_t g = gbase + sp;
-            const uint32_t cnt = cand.count[g];
-            if (cnt > cand.cap) return slow_cut(fp, tab, d, n, s);
-            const uint32_t *P = cand.pos + g * cand.cap;
-            const uint64_t *H = cand.hash + g * cand.cap;
-            const uint64_t sp0 = sp << st.span_log2;
-            uint32_t k = 0;
-            if (lo > sp0) {
-                const uint32_t target = (uint32_t)(lo - sp0);
-                uint32_t l = 0, r = cnt;
-                while (l < r) {
-                    const uint32_t m = (l + r) >> 1;
-                    if (P[m] < target) l = m + 1; else r = m;
+
+    // End offset of the chunk that starts at s.
+    __device__ uint64_t next_cut(uint64_t s) {
+        uint64_t rem = n - s;
+        if (rem <= fp.min) return n;  // tail chunk
+        uint64_t center = fp.avg;
+        if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
+        const uint64_t a0 = (fp.min / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
+        const uint64_t tl = min(a0 + (uint64_t)fp.trunc, re);
+        // (1) Positions s+a0 .. s+tl-1, where the in-chunk hash (reset at s+a0)
+        // still differs from the windowed one: exact recompute from <=47 bytes
+        // staged by four 16-byte loads issued together.
+        if (tl > a0) {
+            const uint64_t w0 = s + a0;
+            const uint64_t al = w0 & ~15ull;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t blk = al + 16 * q;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (blk + 16 <= n) {
+                    v = ld16(as_global4(data + blk));
+                } else if (blk < n) {
+                    g_u8 *gb = as_global1(data);
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (uint64_t j = 0; blk + j < n; ++j) w[j >> 2] |= (uint32_t)gb[blk + j] << (8 * (j & 3));
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                k = l;
+                *reinterpret_cast<uint4 *>(win + 16 * q) = v;
             }
-            for (; k < cnt; ++k) {
-                const uint64_t c = sp0 + P[k];
-                if (c >= hi) return s + rem;
-                if (!(H[k] & ((c - s) < ce ? fp.mask_s : fp.mask_l))) return c;
+            const uint32_t r = (uint32_t)(w0 - al);
+            uint64_t h = 0;
+            for (uint64_t p = a0; p < tl; ++p) {
+                h = (h << 1) + tab[win[r + (uint32_t)(p - a0)]];
+                if (!(h & (p < ce ? fp.mask_s : fp.mask_l))) return s + p;
             }
         }
+        if (tl >= re) return s + rem;
+        // (2) Positions s+tl .. s+re-1: the scan's candidates (flags = exact
+        // mask_s / mask_l tests of the windowed hash).
+        const uint64_t lo = s + tl, hi = s + re;
+        const uint32_t L = st.span_log2;
+        if (cur_sp == ~0ull || cur_sp < (lo >> L)) {
+            cur_sp = lo >> L;
+            cur_k = 0;
+        }
+        while ((cur_sp << L) < hi) {
+            const uint64_t g = gbase + cur_sp;
+            const uint32_t cnt = cand.count[g];
+            if (cnt > cand.cap) return slow_cut(s);
+            const uint32_t *P = cand.pos + g * cand.cap;
+            const uint64_t sp0 = cur_sp << L;
+            for (; cur_k < cnt; ++cur_k) {
+                const uint32_t rec = P[cur_k];
+                const uint64_t c = sp0 + (rec & kCandPosMask);
+                if (c >= hi) return s + rem;
+                if (c >= lo && (rec & ((c - s) < ce ? kCandHitS : kCandHitL))) return c;
+            }
+            ++cur_sp;
+            cur_k = 0;
+        }
+        return s + rem;  // max (or end of data)
     }
-    return s + rem;                                // max (or end of data)
-}
+};
 
 __device__ __forceinline__ void load_tab1(uint64_t *tab, const uint64_t *gear) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = gear[i];
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void spec_kernel(
+// Walk span g's chain from `e` (first chunk start >= span start) until it
+// reaches the span end or merges with the stored chain `old` (whose exit is
+// `old_exit`).  Writes the new chain to `nl`; returns the exit.
+__device__ uint64_t rewalk(Walker &w, uint64_t e, uint64_t seg_end, const uint64_t *old,
+                           uint32_t ocnt, uint64_t old_exit, uint64_t *nl, uint32_t &cnt) {
+    uint32_t j = 0;
+    uint64_t s = e;
+    cnt = 0;
+    for (;;) {
+        if (s >= seg_end) return s;
+        while (j < ocnt && old[j] < s) ++j;
+        if (j < ocnt && old[j] == s) {  // merged: the rest of the old chain holds
+            for (; j < ocnt; ++j) nl[cnt++] = old[j];
+            return old_exit;
+        }
+        nl[cnt++] = s;
+        s = w.next_cut(s);
+    }
+}
+
+__global__ __launch_bounds__(kResolveThreads) void spec_kernel(
     const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
-    const Candidates cand, const Chains ch) {
+    const Candidates cand, const Chains ch, uint64_t *stats) {
     __shared__ uint64_t tab[256];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kResolveThreads * kWin];
     load_tab1(tab, gear);
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g == 0) {
+        for (int i = 0; i < 3; ++i) ch.changed[i] = 0;
+        for (int i = 0; i < 4; ++i) stats[i] = 0;
+    }
     if (g >= st.total_spans) return;
     uint32_t si;
     uint64_t off;
     locate(st, g, si, off);
-    const uint8_t *d = st.ptrs[si];
-    const uint64_t n = st.lens[si], gbase = st.span_base[si];
-    const uint64_t seg_end = min(off + (1ull << st.span_log2), n);
+    Walker w{st, fp, cand, tab, wins + threadIdx.x * kWin, st.ptrs[si], st.lens[si], st.span_base[si]};
+    const uint64_t seg_end = min(off + (1ull << st.span_log2), w.n);
     uint64_t *list = ch.starts[0] + g * ch.smax;
     uint32_t cnt = 0;
     uint64_t s = off;
     while (s < seg_end) {
         list[cnt++] = s;
-        s = next_cut(st, fp, cand, tab, d, n, gbase, s);
+        s = w.next_cut(s);
     }
     ch.nstarts[0][g] = cnt;
     ch.which[g] = 0;
@@ -321,13 +469,26 @@ __global__ __launch_bounds__(256) void spec_kernel(
     ch.exit[0][g] = s;
 }
 
-// One Jacobi pass: reads exits from buffer `b`, writes buffer 1-b.
-__global__ __launch_bounds__(256) void fixup_kernel(
+// Jacobi pass `iter`: reads exits from buffer iter&1, writes the other one.
+// Exits early (writing a 0 flag) once the previous pass changed nothing, so a
+// fixed number of launches needs no host round trip.
+__global__ __launch_bounds__(kResolveThreads) void fixup_kernel(
     const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
-    const Candidates cand, const Chains ch, int b) {
+    const Candidates cand, const Chains ch, int iter, uint64_t *stats) {
     __shared__ uint64_t tab[256];
-    load_tab1(tab, gear);
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kResolveThreads * kWin];
+    uint32_t *flag = ch.changed;
+    const int b = iter & 1;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (iter > 0 && flag[(iter - 1) % 3] == 0) {  // converged: propagate "no change"
+        if (g == 0) flag[iter % 3] = 0;
+        return;
+    }
+    if (g == 0) {
+        flag[(iter + 1) % 3] = 0;
+        atomicAdd((unsigned long long *)&stats[2], 1ull);
+    }
+    load_tab1(tab, gear);
     if (g >= st.total_spans) return;
     uint32_t si;
     uint64_t off;
@@ -342,31 +503,56 @@ __global__ __launch_bounds__(256) void fixup_kernel(
         ch.exit[1 - b][g] = ein;
         return;
     }
-    const uint8_t *d = st.ptrs[si];
-    const uint64_t n = st.lens[si], gbase = st.span_base[si];
-    const uint64_t seg_end = min(off + (1ull << st.span_log2), n);
-    const int w = ch.which[g];
-    const uint64_t *old = ch.starts[w] + g * ch.smax;
-    const uint32_t ocnt = ch.nstarts[w][g];
-    uint64_t *nl = ch.starts[1 - w] + g * ch.smax;
-    uint32_t cnt = 0, j = 0;
-    uint64_t s = e, ex;
-    for (;;) {
-        if (s >= seg_end) { ex = s; break; }
-        while (j < ocnt && old[j] < s) ++j;
-        if (j < ocnt && old[j] == s) {  // merged with the previous chain
-            for (; j < ocnt; ++j) nl[cnt++] = old[j];
-            ex = ein;
-            break;
-        }
-        nl[cnt++] = s;
-        s = next_cut(st, fp, cand, tab, d, n, gbase, s);
-    }
-    ch.nstarts[1 - w][g] = cnt;
-    ch.which[g] = (uint8_t)(1 - w);
+    Walker w{st, fp, cand, tab, wins + threadIdx.x * kWin, st.ptrs[si], st.lens[si], st.span_base[si]};
+    const uint64_t seg_end = min(off + (1ull << st.span_log2), w.n);
+    const int wb = ch.which[g];
+    uint32_t cnt;
+    const uint64_t ex = rewalk(w, e, seg_end, ch.starts[wb] + g * ch.smax, ch.nstarts[wb][g], ein,
+                               ch.starts[1 - wb] + g * ch.smax, cnt);
+    ch.nstarts[1 - wb][g] = cnt;
+    ch.which[g] = (uint8_t)(1 - wb);
     ch.entry[g] = e;
     ch.exit[1 - b][g] = ex;
-    if (ex != ein) atomicOr(ch.changed, 1u);
+    if (ex != ein) atomicOr(&flag[iter % 3], 1u);
+}
+
+// Serial catch-up, one thread per stream, after the Jacobi passes: a no-op
+// unless the last pass still changed an exit (chains that do not merge within
+// a span, e.g. long runs of max-length cuts in constant data).  Then it walks
+// the stream's spans in order, re-walking only spans whose entry is stale:
+// exact in one pass, O(stale chunks) steps.
+__global__ __launch_bounds__(kResolveThreads) void serial_kernel(
+    const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
+    const Candidates cand, const Chains ch, int buf, int slot, uint64_t *stats) {
+    __shared__ uint64_t tab[256];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kResolveThreads * kWin];
+    if (ch.changed[slot] == 0) return;
+    load_tab1(tab, gear);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= st.n) return;
+    if (i == 0) stats[3] = 1;
+    const uint64_t g0 = st.span_base[i], g1 = st.span_base[i + 1];
+    if (g1 - g0 < 2) return;
+    Walker w{st, fp, cand, tab, wins + threadIdx.x * kWin, st.ptrs[i], st.lens[i], g0};
+    uint64_t prev = ch.exit[buf][g0];
+    for (uint64_t g = g0 + 1; g < g1; ++g) {
+        if (prev == ch.entry[g]) {
+            prev = ch.exit[buf][g];
+            continue;
+        }
+        const uint64_t off = (g - g0) << st.span_log2;
+        const uint64_t seg_end = min(off + (1ull << st.span_log2), w.n);
+        const int wb = ch.which[g];
+        uint32_t cnt;
+        w.cur_sp = ~0ull;
+        const uint64_t ex = rewalk(w, prev, seg_end, ch.starts[wb] + g * ch.smax, ch.nstarts[wb][g],
+                                   ch.exit[buf][g], ch.starts[1 - wb] + g * ch.smax, cnt);
+        ch.nstarts[1 - wb][g] = cnt;
+        ch.which[g] = (uint8_t)(1 - wb);
+        ch.entry[g] = prev;
+        ch.exit[buf][g] = ex;
+        prev = ex;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -523,19 +709,28 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp,
 
 hipError_t launch_spec(const StreamTable &st, const FastParams &fp,
                        const uint64_t *d_gear, const Candidates &cand,
-                       const Chains &ch, hipStream_t s) {
+                       const Chains &ch, uint64_t *stats, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (unsigned)((st.total_spans + 255) / 256);
-    spec_kernel<<<grid, 256, 0, s>>>(st, fp, d_gear, cand, ch);
+    const unsigned grid = (unsigned)((st.total_spans + kResolveThreads - 1) / kResolveThreads);
+    spec_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, ch, stats);
     return hipGetLastError();
 }
 
 hipError_t launch_fixup(const StreamTable &st, const FastParams &fp,
                         const uint64_t *d_gear, const Candidates &cand,
-                        const Chains &ch, int in_buf, hipStream_t s) {
+                        const Chains &ch, int iter, uint64_t *stats, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (unsigned)((st.total_spans + 255) / 256);
-    fixup_kernel<<<grid, 256, 0, s>>>(st, fp, d_gear, cand, ch, in_buf);
+    const unsigned grid = (unsigned)((st.total_spans + kResolveThreads - 1) / kResolveThreads);
+    fixup_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, ch, iter, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_serial(const StreamTable &st, const FastParams &fp,
+                         const uint64_t *d_gear, const Candidates &cand,
+                         const Chains &ch, int buf, int slot, uint64_t *stats, hipStream_t s) {
+    if (!st.total_spans) return hipSuccess;
+    const unsigned grid = (st.n + kResolveThreads - 1) / kResolveThreads;
+    serial_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, ch, buf, slot, stats);
     return hipGetLastError();
 }
 

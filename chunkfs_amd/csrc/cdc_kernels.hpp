@@ -48,9 +48,8 @@ struct FastParams {
 
 struct Candidates {
     uint32_t cap;
-    uint32_t *count;  // [spans]
-    uint32_t *pos;    // [spans*cap]
-    uint64_t *hash;   // [spans*cap]
+    uint32_t *count;  // [spans]: candidates found (> cap = overflowed)
+    uint32_t *pos;    // [spans*cap]: offset in span | bit30 mask_l hit | bit31 mask_s hit
 };
 
 struct Chains {
@@ -60,13 +59,13 @@ struct Chains {
     uint8_t *which;        // [spans]
     uint64_t *entry;       // [spans]
     uint64_t *exit[2];     // [spans]
-    uint32_t *changed;     // [1]
+    uint32_t *changed;     // [3]: rotating "some exit changed" flags of the Jacobi passes
 };
 
 struct Compact {
     uint64_t *chunk_index;   // [spans+1]
     uint64_t *block_sums;    // [ceil(spans/1024)+1]
-    uint64_t *stats;         // [2]: candidates, overflow spans
+    uint64_t *stats;         // [4]: candidates, overflow spans, Jacobi passes run, serial used
     uint64_t *first;         // [n+1]
 };
 
@@ -75,10 +74,14 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp,
                        int num_cus, hipStream_t s);
 hipError_t launch_spec(const StreamTable &st, const FastParams &fp,
                        const uint64_t *d_gear, const Candidates &cand,
-                       const Chains &ch, hipStream_t s);
+                       const Chains &ch, uint64_t *stats, hipStream_t s);
 hipError_t launch_fixup(const StreamTable &st, const FastParams &fp,
                         const uint64_t *d_gear, const Candidates &cand,
-                        const Chains &ch, int in_buf, hipStream_t s);
+                        const Chains &ch, int iter, uint64_t *stats, hipStream_t s);
+hipError_t launch_serial(const StreamTable &st, const FastParams &fp,
+                         const uint64_t *d_gear, const Candidates &cand,
+                         const Chains &ch, int buf, int slot, uint64_t *stats,
+                         hipStream_t s);
 hipError_t launch_compact(const StreamTable &st, const Chains &ch,
                           int exit_buf, const Candidates &cand,
                           const Compact &cp, void *d_out, hipStream_t s);

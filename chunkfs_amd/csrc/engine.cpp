@@ -101,7 +101,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         const uint32_t pc = (uint32_t)__builtin_popcountll(fp.cmask);
         uint64_t cap = 8 * (span >> (pc < 63 ? pc : 63));
         if (cap < 64) cap = 64;
-        if (cap > span) cap = span;
+        if (cap > 256) cap = 256;
         e->cap_ = (uint32_t)cap;
         e->smax_ = (uint32_t)(span / ((min / 2) * 2) + 2);
         char buf[256];
@@ -210,18 +210,19 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
         off = align_up(off + bytes, A);
         return o;
     };
-    const size_t o_count = take(S * 4), o_pos = take(S * cap * 4), o_hash = take(S * cap * 8);
+    const size_t o_count = take(S * 4), o_pos = take(S * cap * 4);
     const size_t o_st0 = take(S * smax * 8), o_st1 = take(S * smax * 8);
     const size_t o_ns0 = take(S * 4), o_ns1 = take(S * 4), o_which = take(S);
     const size_t o_entry = take(S * 8), o_ex0 = take(S * 8), o_ex1 = take(S * 8);
-    const size_t o_changed = take(8), o_ci = take((S + 1) * 8);
-    const size_t o_bs = take((S / 1024 + 2) * 8), o_stats = take(16), o_first = take((N + 1) * 8);
+    const size_t o_changed = take(16), o_ci = take((S + 1) * 8);
+    const size_t o_bs = take((S / 1024 + 2) * 8), o_stats = take(32), o_first = take((N + 1) * 8);
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
     ws_spans_ = 0;
     ws_streams_ = 0;
     HIP_TRY(hipMalloc(&ws_, off));
+    ++ws_gen_;
     ws_bytes_ = off;
     ws_spans_ = S;
     ws_streams_ = N;
@@ -229,7 +230,6 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     cand_.cap = (uint32_t)cap;
     cand_.count = reinterpret_cast<uint32_t *>(b + o_count);
     cand_.pos = reinterpret_cast<uint32_t *>(b + o_pos);
-    cand_.hash = reinterpret_cast<uint64_t *>(b + o_hash);
     chains_.smax = (uint32_t)smax;
     chains_.starts[0] = reinterpret_cast<uint64_t *>(b + o_st0);
     chains_.starts[1] = reinterpret_cast<uint64_t *>(b + o_st1);
@@ -306,9 +306,19 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     }
     rc = ensure_workspace(spans, n);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(d_ptrs_, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_lens_, h_lens, n * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_span_base_, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    // The three per-stream tables are re-uploaded only when they change
+    // (repeated batches over the same device buffers skip the H2D copies).
+    const bool same = ws_gen_ == tables_gen_ && tables_.size() == 2 * n &&
+                      std::memcmp(tables_.data(), h_ptrs, n * 8) == 0 &&
+                      std::memcmp(tables_.data() + n, h_lens, n * 8) == 0;
+    if (!same) {
+        HIP_TRY(hipMemcpyAsync(d_ptrs_, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_lens_, h_lens, n * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_span_base_, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
+        tables_.assign(h_ptrs, h_ptrs + n);
+        tables_.insert(tables_.end(), h_lens, h_lens + n);
+        tables_gen_ = ws_gen_;
+    }
     StreamTable st{};
     st.ptrs = d_ptrs_;
     st.lens = d_lens_;
@@ -326,32 +336,26 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                      uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_first = h + 3 * h_stage_streams_;
-    uint64_t *h_misc = h + 4 * h_stage_streams_;  // [0] flag, [1..2] stats
+    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats[4] + changed flags
     HIP_TRY(hipEventRecord(ev_[0], s));
     HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
-    HIP_TRY(launch_spec(st, fp_, d_gear_, cand_, chains_, s));
-    int b = 0;
-    uint32_t iters = 0;
-    const bool multi = st.total_spans > st.n;  // some stream has >= 2 spans
-    while (multi) {
-        HIP_TRY(hipMemsetAsync(chains_.changed, 0, 4, s));
-        HIP_TRY(launch_fixup(st, fp_, d_gear_, cand_, chains_, b, s));
-        b ^= 1;
-        ++iters;
-        HIP_TRY(hipMemcpyAsync(h_misc, chains_.changed, 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (*reinterpret_cast<volatile uint32_t *>(h_misc) == 0) break;
-        if (iters > st.total_spans + 2) {
-            set_error("resolve did not converge (internal error)");
-            return CDC_EDEVICE;
-        }
+    HIP_TRY(launch_spec(st, fp_, d_gear_, cand_, chains_, comp_.stats, s));
+    int exit_buf = 0;
+    if (st.total_spans > st.n) {  // some stream has >= 2 spans: chains must be joined
+        // kJacobi device passes (each a no-op once converged) and a serial
+        // catch-up that runs only if the last pass still changed an exit: no
+        // host round trip on any path.
+        for (int it = 0; it < kJacobi; ++it)
+            HIP_TRY(launch_fixup(st, fp_, d_gear_, cand_, chains_, it, comp_.stats, s));
+        exit_buf = kJacobi & 1;
+        HIP_TRY(launch_serial(st, fp_, d_gear_, cand_, chains_, exit_buf, (kJacobi - 1) % 3,
+                              comp_.stats, s));
     }
     HIP_TRY(hipEventRecord(ev_[2], s));
-    HIP_TRY(hipMemsetAsync(comp_.stats, 0, 16, s));
-    HIP_TRY(launch_compact(st, chains_, b, cand_, comp_, d_out, s));
+    HIP_TRY(launch_compact(st, chains_, exit_buf, cand_, comp_, d_out, s));
     HIP_TRY(hipMemcpyAsync(h_first, comp_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h_misc + 1, comp_.stats, 16, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_misc, comp_.stats, 32, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ev_[3], s));
     HIP_TRY(hipStreamSynchronize(s));
     std::memcpy(first, h_first, (n + 1) * 8);
@@ -364,9 +368,9 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     timing_.resolve_ms = t12;
     timing_.compact_ms = t23;
     timing_.total_ms = t03;
-    timing_.fixup_iterations = iters;
-    timing_.candidates = h_misc[1];
-    timing_.overflow_spans = (uint32_t)h_misc[2];
+    timing_.candidates = h_misc[0];
+    timing_.overflow_spans = (uint32_t)h_misc[1];
+    timing_.fixup_iterations = (uint32_t)h_misc[2] + (h_misc[3] ? 1000u : 0u);
     return CDC_OK;
 }
 

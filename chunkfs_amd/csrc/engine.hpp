@@ -85,6 +85,13 @@ class Engine {
     size_t d_out_cap_ = 0;
 
     cdc_timing_t timing_{};
+
+    // Last uploaded stream tables (ptrs ++ lens) and the workspace generation
+    // they were uploaded into.
+    std::vector<uint64_t> tables_;
+    uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
+
+    static constexpr int kJacobi = 3;  // device-side Jacobi passes per batch
 };
 
 void set_error(const std::string &msg);

@@ -1,0 +1,33 @@
+#!/bin/bash
+# PMC passes on the scan kernel (separate rocprofv3 runs, counters only, as
+# MI355X_MICROARCH.md prescribes).  Usage: tools/pmc.sh TAG
+TAG=${1:-r01}
+OUT=gpurun_out/pmc_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
+run() {  # name, counters...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "scan_kernel" --output-format csv \
+      -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity \
+      > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "pmc $name rc=$rc"
+  return $rc
+}
+ok() { [ $1 -eq 0 ] || [ $1 -eq 1 ]; }
+run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY; ok $? || exit 1
+run sq2 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT; ok $? || exit 1
+run fetch FETCH_SIZE; ok $? || exit 1
+run tcc TCC_HIT_sum TCC_MISS_sum; ok $? || exit 1
+for d in $OUT/*/; do f=$(find $d -name "*counter_collection.csv" | head -1); [ -n "$f" ] && echo "== $d" && python3 - "$f" <<'PY'
+import csv, sys, collections
+rows = list(csv.DictReader(open(sys.argv[1])))
+agg = collections.defaultdict(list)
+for r in rows:
+    agg[r.get("Counter_Name")].append(float(r.get("Counter_Value", 0)))
+for k, v in agg.items():
+    print(f"{k}: n={len(v)} mean={sum(v)/len(v):.4g} min={min(v):.4g} max={max(v):.4g}")
+PY
+done
+exit 0
