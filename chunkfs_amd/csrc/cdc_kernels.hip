@@ -39,6 +39,12 @@ constexpr uint32_t kEntCap = 64;      // per-wave LDS list of hitting 16-byte qu
 constexpr uint32_t kCandPosMask = 0x00FFFFFFu;
 constexpr uint32_t kCandHitL = 1u << 30;
 constexpr uint32_t kCandHitS = 1u << 31;
+// Bits 24..29: truncated-region result of the chunk starting at the record
+// (written by trunc_kernel): 0..46 = first hitting offset after start+a0.
+constexpr uint32_t kCandTrShift = 24;
+constexpr uint32_t kCandTrMask = 0x3Fu;
+constexpr uint32_t kCandTrNone = 62;
+constexpr uint32_t kCandTrUnk = 63;
 
 // Global (address space 1) views of the stream bytes.  Generic pointers would
 // compile to flat_load_*, which count on both vmcnt and lgkmcnt and may return
@@ -315,43 +321,160 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Resolve.  One thread walks one chain; `tab` is a single LDS copy of GEAR and
-// `win` the thread's 64-byte LDS window for the truncated-hash check.
+// Resolve (wave-cooperative).  One wavefront walks one chain; every branch
+// below is wave-uniform.
+//
+// A chunk starting at s is cut at the first position p in [s+a0, s+re) whose
+// in-chunk hash (reset at s+a0) hits its mask.  Two kinds of positions:
+//  * the <= 47 "truncated" positions s+a0 .. s+a0+46, where that hash still
+//    differs from the windowed one: evaluated exactly, either precomputed per
+//    candidate record (a lane per record, when its span is loaded) or, for
+//    chunks that do not start at a record, by one coalesced byte load + a
+//    6-step shuffle prefix scan;
+//  * all later positions: the scan's candidate records (position-sorted, one
+//    per lane), tested with a ballot.
+// So a walk step that starts at a record -- about 90% of them -- touches no
+// memory.
 
-constexpr int kResolveThreads = 256;
-constexpr uint32_t kWin = 64;
+constexpr int kResolveThreads = 256;  // 4 waves: one span (or stream) each
+constexpr int kResolveWaves = kResolveThreads / 64;
+constexpr uint32_t kTrUnk = 0xFF;   // truncated result not precomputed
+constexpr uint32_t kTrNone = 0xFE;  // precomputed: no hit in the truncated region
+constexpr uint32_t kTruncMax = 47;  // mask bits <= 47 (checked on the host)
 
-struct Walker {
+// Inclusive scan of the gear recurrence across lanes:
+// lane d returns sum_{i<=d} g_i << (d - i)  (mod 2^64).
+__device__ __forceinline__ uint64_t gear_prefix(uint64_t g, uint32_t lane) {
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+        const uint64_t t = __shfl_up(g, k);
+        if (lane >= (uint32_t)k) g += t << k;
+    }
+    return g;
+}
+
+typedef const __attribute__((address_space(1))) uint32_t g_u32;
+
+// Dword at byte offset `off` (4-aligned) of a stream of n bytes, zero past n.
+__device__ __forceinline__ uint32_t ld4_guarded(const uint8_t *data, uint64_t off, uint64_t n) {
+    if (off + 4 <= n) return *(g_u32 *)(data + off);
+    uint32_t w = 0;
+    g_u8 *gb = as_global1(data);
+    for (uint64_t j = 0; off + j < n; ++j) w |= (uint32_t)gb[off + j] << (8 * j);
+    return w;
+}
+
+struct SpanRecs {
+    uint32_t cnt = 0;   // records in the span (> cap: overflowed)
+    uint32_t rec = 0;   // record `lane` (records 0..63)
+    uint32_t tr = kTrUnk;
+};
+
+struct WaveWalker {
     const StreamTable &st;
     const FastParams &fp;
     const Candidates &cand;
-    const uint64_t *tab;
-    uint8_t *win;
+    const uint64_t *tab;  // LDS GEAR (one copy)
     const uint8_t *data;
     uint64_t n;
     uint64_t gbase;
-    // Monotonic candidate cursor: along one chain every window starts after
-    // the previous one, so each candidate record is read at most once.
-    uint64_t cur_sp = ~0ull;
-    uint32_t cur_k = 0;
+    uint32_t lane;
+    // Spans ra and ra+1 are resident (the search window of a chunk is at most
+    // max <= SPAN bytes, so it touches at most two spans).  The walk only
+    // moves forward: each span is fetched once.
+    uint64_t ra = ~0ull;
+    bool hb = false;
+    SpanRecs A, B;
+    uint64_t last_cut = ~0ull;  // last cut that came from a record ...
+    uint32_t last_t = kTrUnk;   // ... and that record's truncated result
 
-    // Exact sequential cut (byte-wise form of cut_gear); used
-    // only when a span's candidate list overflowed (low-entropy data).
-    __device__ uint64_t slow_cut(uint64_t s) {
-        g_u8 *d = as_global1(data);
-        uint64_t rem = n - s;
-        uint64_t center = fp.avg;
-        if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
-        const uint64_t a0 = (fp.min / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
+    __device__ SpanRecs fetch(uint64_t sp) {
+        SpanRecs R;
+        if ((sp << st.span_log2) >= n) return R;  // past the stream's last span
+        const uint64_t g = gbase + sp;
+        // Count and record slot `lane` are loaded together (cap >= 64): one
+        // round trip per span.
+        R.cnt = cand.count[g];
+        const uint32_t raw = cand.pos[g * cand.cap + lane];
+        if (R.cnt > cand.cap || R.cnt == 0) return R;
+        R.rec = lane < R.cnt ? raw : 0;
+        const uint32_t t = (R.rec >> kCandTrShift) & kCandTrMask;  // from trunc_kernel
+        R.tr = t == kCandTrUnk ? kTrUnk : t == kCandTrNone ? kTrNone : t;
+        return R;
+    }
+    __device__ void ensure_a(uint64_t sp) {
+        if (ra == sp) return;
+        if (hb && ra + 1 == sp) {
+            A = B;
+        } else {
+            A = fetch(sp);
+        }
+        ra = sp;
+        hb = false;
+    }
+    __device__ void ensure_b() {
+        if (!hb) {
+            B = fetch(ra + 1);
+            hb = true;
+        }
+    }
+
+    // Exact hashes at positions s+p, p in [p0, p1) (p1 - p0 <= 64), chained
+    // from `hin` = hash at s+p0-1 (0 = reset).  Returns the first relative
+    // position that hits its mask (~0 if none); hout = hash at s+p1-1.
+    __device__ uint64_t block_hits(uint64_t s, uint64_t p0, uint64_t p1, uint64_t ce,
+                                   uint64_t hin, uint64_t &hout) {
+        const uint64_t p = p0 + lane;
+        const bool in = p < p1;
+        uint64_t gv = 0;
+        if (in) gv = tab[as_global1(data)[s + p]];
+        uint64_t x = gear_prefix(gv, lane) + ((hin << lane) << 1);
+        const bool hit = in && !(x & (p < ce ? fp.mask_s : fp.mask_l));
+        const uint64_t m = __ballot(hit);
+        hout = __shfl(x, (int)(p1 - p0 - 1));
+        return m ? p0 + (uint64_t)(__ffsll((long long)m) - 1) : ~0ull;
+    }
+
+    // Exact scan of [a0, re) in 64-position blocks (overflowed candidate list).
+    __device__ uint64_t slow_cut(uint64_t s, uint64_t a0, uint64_t re, uint64_t ce, uint64_t rem) {
         uint64_t h = 0;
-        for (uint64_t p = a0; p < re; ++p) {
-            h = (h << 1) + tab[d[s + p]];
-            if (!(h & (p < ce ? fp.mask_s : fp.mask_l))) return s + p;
+        for (uint64_t b = a0; b < re; b += 64) {
+            const uint64_t p = block_hits(s, b, min(b + 64, re), ce, h, h);
+            if (p != ~0ull) return s + p;
         }
         return s + rem;
     }
 
-    // End offset of the chunk that starts at s.
+    // Search span sp's records for the first hit in [lo, hi).  Returns the cut,
+    // s+rem when a record at or past hi proves there is none, or ~0 to go on
+    // with the next span.
+    __device__ uint64_t search(uint64_t sp, const SpanRecs &R, uint64_t s, uint64_t lo,
+                               uint64_t hi, uint64_t ce, uint64_t rem, bool &ovf) {
+        if (R.cnt > cand.cap) {
+            ovf = true;
+            return ~0ull;
+        }
+        const uint64_t sp0 = sp << st.span_log2;
+        const uint32_t *P = cand.pos + (gbase + sp) * cand.cap;
+        for (uint32_t base = 0; base < R.cnt; base += 64) {
+            const bool have = base + lane < R.cnt;
+            uint32_t r = R.rec;
+            if (base) r = have ? P[base + lane] : 0;
+            const uint64_t c = sp0 + (r & kCandPosMask);
+            const bool ok = have && c >= lo && c < hi && (r & ((c - s) < ce ? kCandHitS : kCandHitL));
+            const uint64_t mo = __ballot(ok);
+            if (mo) {  // position-sorted: the lowest lane is the first hit
+                const int k = __ffsll((long long)mo) - 1;
+                last_cut = __shfl(c, k);
+                last_t = base == 0 ? (uint32_t)__shfl((int)R.tr, k) : kTrUnk;
+                return last_cut;
+            }
+            if (__ballot(have && c >= hi)) return s + rem;
+        }
+        return ~0ull;
+    }
+
+    // End offset of the chunk that starts at s (SURVEY.md A.2 semantics).
     __device__ uint64_t next_cut(uint64_t s) {
         uint64_t rem = n - s;
         if (rem <= fp.min) return n;  // tail chunk
@@ -359,58 +482,25 @@ struct Walker {
         if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
         const uint64_t a0 = (fp.min / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
         const uint64_t tl = min(a0 + (uint64_t)fp.trunc, re);
-        // (1) Positions s+a0 .. s+tl-1, where the in-chunk hash (reset at s+a0)
-        // still differs from the windowed one: exact recompute from <=47 bytes
-        // staged by four 16-byte loads issued together.
-        if (tl > a0) {
-            const uint64_t w0 = s + a0;
-            const uint64_t al = w0 & ~15ull;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t blk = al + 16 * q;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (blk + 16 <= n) {
-                    v = ld16(as_global4(data + blk));
-                } else if (blk < n) {
-                    g_u8 *gb = as_global1(data);
-                    uint32_t w[4] = {0, 0, 0, 0};
-                    for (uint64_t j = 0; blk + j < n; ++j) w[j >> 2] |= (uint32_t)gb[blk + j] << (8 * (j & 3));
-                    v = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-                *reinterpret_cast<uint4 *>(win + 16 * q) = v;
-            }
-            const uint32_t r = (uint32_t)(w0 - al);
-            uint64_t h = 0;
-            for (uint64_t p = a0; p < tl; ++p) {
-                h = (h << 1) + tab[win[r + (uint32_t)(p - a0)]];
-                if (!(h & (p < ce ? fp.mask_s : fp.mask_l))) return s + p;
-            }
+        if (s == last_cut && last_t != kTrUnk) {  // precomputed with the record
+            if (last_t != kTrNone) return s + a0 + last_t;
+        } else if (tl > a0) {
+            uint64_t h;
+            const uint64_t p = block_hits(s, a0, tl, ce, 0, h);
+            if (p != ~0ull) return s + p;
         }
         if (tl >= re) return s + rem;
-        // (2) Positions s+tl .. s+re-1: the scan's candidates (flags = exact
-        // mask_s / mask_l tests of the windowed hash).
         const uint64_t lo = s + tl, hi = s + re;
-        const uint32_t L = st.span_log2;
-        if (cur_sp == ~0ull || cur_sp < (lo >> L)) {
-            cur_sp = lo >> L;
-            cur_k = 0;
+        const uint64_t sl = lo >> st.span_log2;
+        bool ovf = false;
+        ensure_a(sl);
+        uint64_t r = search(sl, A, s, lo, hi, ce, rem, ovf);
+        if (r == ~0ull && !ovf && ((sl + 1) << st.span_log2) < hi) {
+            ensure_b();
+            r = search(sl + 1, B, s, lo, hi, ce, rem, ovf);
         }
-        while ((cur_sp << L) < hi) {
-            const uint64_t g = gbase + cur_sp;
-            const uint32_t cnt = cand.count[g];
-            if (cnt > cand.cap) return slow_cut(s);
-            const uint32_t *P = cand.pos + g * cand.cap;
-            const uint64_t sp0 = cur_sp << L;
-            for (; cur_k < cnt; ++cur_k) {
-                const uint32_t rec = P[cur_k];
-                const uint64_t c = sp0 + (rec & kCandPosMask);
-                if (c >= hi) return s + rem;
-                if (c >= lo && (rec & ((c - s) < ce ? kCandHitS : kCandHitL))) return c;
-            }
-            ++cur_sp;
-            cur_k = 0;
-        }
-        return s + rem;  // max (or end of data)
+        if (ovf) return slow_cut(s, a0, re, ce, rem);
+        return r == ~0ull ? s + rem : r;  // none: max (or end of data)
     }
 };
 
@@ -420,33 +510,106 @@ __device__ __forceinline__ void load_tab1(uint64_t *tab, const uint64_t *gear) {
 }
 
 // Walk span g's chain from `e` (first chunk start >= span start) until it
-// reaches the span end or merges with the stored chain `old` (whose exit is
+// reaches the span end or merges with the stored chain `old` (exit
 // `old_exit`).  Writes the new chain to `nl`; returns the exit.
-__device__ uint64_t rewalk(Walker &w, uint64_t e, uint64_t seg_end, const uint64_t *old,
+__device__ uint64_t rewalk(WaveWalker &w, uint64_t e, uint64_t seg_end, const uint64_t *old,
                            uint32_t ocnt, uint64_t old_exit, uint64_t *nl, uint32_t &cnt) {
-    uint32_t j = 0;
+    const uint32_t lane = w.lane;
+    uint32_t j0 = 0;
     uint64_t s = e;
     cnt = 0;
     for (;;) {
         if (s >= seg_end) return s;
-        while (j < ocnt && old[j] < s) ++j;
-        if (j < ocnt && old[j] == s) {  // merged: the rest of the old chain holds
-            for (; j < ocnt; ++j) nl[cnt++] = old[j];
-            return old_exit;
+        for (;;) {  // is s on the old chain?  (old is sorted)
+            const uint32_t k = j0 + lane;
+            const uint64_t o = k < ocnt ? old[k] : ~0ull;
+            const uint64_t meq = __ballot(o == s);
+            if (meq) {  // merged: the rest of the old chain holds
+                const uint32_t j = j0 + (uint32_t)(__ffsll((long long)meq) - 1);
+                for (uint32_t t = lane; j + t < ocnt; t += 64) nl[cnt + t] = old[j + t];
+                cnt += ocnt - j;
+                return old_exit;
+            }
+            const uint32_t nlt = (uint32_t)__popcll(__ballot(k < ocnt && o < s));
+            j0 += nlt;
+            if (nlt < 64) break;
         }
-        nl[cnt++] = s;
+        if (lane == 0) nl[cnt] = s;
+        ++cnt;
         s = w.next_cut(s);
     }
 }
 
+// Truncated region of the chunk that would START at each candidate record:
+// one wave per span, one lane per record.  The result (first hitting offset
+// 0..46, "none", or "unknown" when that chunk's centre is not avg or its
+// region is short -- near the end of a stream) goes into the record's spare
+// bits 24..29, so the walk needs no memory access for chunks that start at a
+// record.  Bytes are staged per lane in LDS (13 dwords, odd stride: no bank
+// conflicts), the 47-step chain reads them back.
+__global__ __launch_bounds__(kResolveThreads) void trunc_kernel(
+    const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
+    const Candidates cand) {
+    __shared__ uint64_t tab[256];
+    __shared__ uint32_t win[kResolveThreads * 13];
+    load_tab1(tab, gear);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * kResolveWaves + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    const uint32_t cnt = cand.count[g];
+    if (cnt > cand.cap) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint8_t *data = st.ptrs[si];
+    const uint64_t n = st.lens[si];
+    const uint64_t a0 = (fp.min / 2) * 2, cavg = (fp.avg / 2) * 2;
+    uint32_t *wl = win + threadIdx.x * 13;
+    for (uint32_t k = lane; k < cnt; k += 64) {
+        uint32_t rec = cand.pos[g * cand.cap + k];
+        const uint64_t c = off + (rec & kCandPosMask);
+        const uint64_t remc = n - c;
+        const uint64_t rr = remc > fp.max ? fp.max : remc;
+        uint32_t t = kCandTrUnk;
+        if (remc > fp.min && remc >= fp.avg && (rr / 2) * 2 >= a0 + fp.trunc) {
+            const uint64_t w0 = c + a0, al = w0 & ~3ull;
+            uint32_t w[13];
+            if (al + 52 <= n) {  // all 13 loads in flight at once
+#pragma unroll
+                for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(data + al + 4 * i);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 13; ++i) w[i] = ld4_guarded(data, al + 4 * i, n);
+            }
+#pragma unroll
+            for (int i = 0; i < 13; ++i) wl[i] = w[i];
+            const uint8_t *bytes = reinterpret_cast<const uint8_t *>(wl) + (w0 - al);
+            uint64_t h = 0;
+            t = kCandTrNone;
+#pragma unroll 8
+            for (uint32_t d = 0; d < kTruncMax; ++d) {  // no early exit: LDS reads pipeline
+                h = shl1_add(h, tab[bytes[d]]);
+                const bool hit = d < fp.trunc && !(h & ((a0 + d) < cavg ? fp.mask_s : fp.mask_l));
+                t = hit ? min(t, d) : t;
+            }
+        }
+        rec = (rec & ~(kCandTrMask << kCandTrShift)) | (t << kCandTrShift);
+        cand.pos[g * cand.cap + k] = rec;
+    }
+}
+
+// Speculative chain of span g.  The walk starts 2*max bytes before the span
+// (exact when that is the stream start), so by the time it reaches span g it
+// has almost always merged with the true chain: the Jacobi passes then find
+// entry[g] == exit[g-1] and do no work.
 __global__ __launch_bounds__(kResolveThreads) void spec_kernel(
     const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
     const Candidates cand, const Chains ch, uint64_t *stats) {
     __shared__ uint64_t tab[256];
-    __shared__ __attribute__((aligned(16))) uint8_t wins[kResolveThreads * kWin];
     load_tab1(tab, gear);
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g == 0) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * kResolveWaves + (threadIdx.x >> 6);
+    if (g == 0 && lane == 0) {
         for (int i = 0; i < 3; ++i) ch.changed[i] = 0;
         for (int i = 0; i < 4; ++i) stats[i] = 0;
     }
@@ -454,19 +617,30 @@ __global__ __launch_bounds__(kResolveThreads) void spec_kernel(
     uint32_t si;
     uint64_t off;
     locate(st, g, si, off);
-    Walker w{st, fp, cand, tab, wins + threadIdx.x * kWin, st.ptrs[si], st.lens[si], st.span_base[si]};
-    const uint64_t seg_end = min(off + (1ull << st.span_log2), w.n);
+    WaveWalker w{st, fp, cand, tab, st.ptrs[si], st.lens[si], st.span_base[si], lane};
+    const uint64_t span = 1ull << st.span_log2;
+    const uint64_t seg_end = min(off + span, w.n);
     uint64_t *list = ch.starts[0] + g * ch.smax;
     uint32_t cnt = 0;
-    uint64_t s = off;
+    // Warm-up start: 2*max before the span (the stream start when closer).
+    const uint64_t warm = 2ull * fp.max;
+    uint64_t s = off > warm ? off - warm : 0;
+    // Both spans the walk begins in, fetched together (one round trip).
+    w.ensure_a(s >> st.span_log2);
+    w.ensure_b();
     while (s < seg_end) {
-        list[cnt++] = s;
+        if (s >= off) {
+            if (lane == 0) list[cnt] = s;
+            ++cnt;
+        }
         s = w.next_cut(s);
     }
-    ch.nstarts[0][g] = cnt;
-    ch.which[g] = 0;
-    ch.entry[g] = off;
-    ch.exit[0][g] = s;
+    if (lane == 0) {
+        ch.nstarts[0][g] = cnt;
+        ch.which[g] = 0;
+        ch.entry[g] = cnt ? list[0] : s;
+        ch.exit[0][g] = s;
+    }
 }
 
 // Jacobi pass `iter`: reads exits from buffer iter&1, writes the other one.
@@ -476,15 +650,15 @@ __global__ __launch_bounds__(kResolveThreads) void fixup_kernel(
     const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
     const Candidates cand, const Chains ch, int iter, uint64_t *stats) {
     __shared__ uint64_t tab[256];
-    __shared__ __attribute__((aligned(16))) uint8_t wins[kResolveThreads * kWin];
     uint32_t *flag = ch.changed;
     const int b = iter & 1;
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * kResolveWaves + (threadIdx.x >> 6);
     if (iter > 0 && flag[(iter - 1) % 3] == 0) {  // converged: propagate "no change"
-        if (g == 0) flag[iter % 3] = 0;
+        if (g == 0 && lane == 0) flag[iter % 3] = 0;
         return;
     }
-    if (g == 0) {
+    if (g == 0 && lane == 0) {
         flag[(iter + 1) % 3] = 0;
         atomicAdd((unsigned long long *)&stats[2], 1ull);
     }
@@ -495,28 +669,30 @@ __global__ __launch_bounds__(kResolveThreads) void fixup_kernel(
     locate(st, g, si, off);
     const uint64_t ein = ch.exit[b][g];
     if (off == 0) {  // first span of a stream: its entry (0) is exact
-        ch.exit[1 - b][g] = ein;
+        if (lane == 0) ch.exit[1 - b][g] = ein;
         return;
     }
     const uint64_t e = ch.exit[b][g - 1];
     if (e == ch.entry[g]) {
-        ch.exit[1 - b][g] = ein;
+        if (lane == 0) ch.exit[1 - b][g] = ein;
         return;
     }
-    Walker w{st, fp, cand, tab, wins + threadIdx.x * kWin, st.ptrs[si], st.lens[si], st.span_base[si]};
+    WaveWalker w{st, fp, cand, tab, st.ptrs[si], st.lens[si], st.span_base[si], lane};
     const uint64_t seg_end = min(off + (1ull << st.span_log2), w.n);
     const int wb = ch.which[g];
     uint32_t cnt;
     const uint64_t ex = rewalk(w, e, seg_end, ch.starts[wb] + g * ch.smax, ch.nstarts[wb][g], ein,
                                ch.starts[1 - wb] + g * ch.smax, cnt);
-    ch.nstarts[1 - wb][g] = cnt;
-    ch.which[g] = (uint8_t)(1 - wb);
-    ch.entry[g] = e;
-    ch.exit[1 - b][g] = ex;
-    if (ex != ein) atomicOr(&flag[iter % 3], 1u);
+    if (lane == 0) {
+        ch.nstarts[1 - wb][g] = cnt;
+        ch.which[g] = (uint8_t)(1 - wb);
+        ch.entry[g] = e;
+        ch.exit[1 - b][g] = ex;
+        if (ex != ein) atomicOr(&flag[iter % 3], 1u);
+    }
 }
 
-// Serial catch-up, one thread per stream, after the Jacobi passes: a no-op
+// Serial catch-up, one wave per stream, after the Jacobi passes: a no-op
 // unless the last pass still changed an exit (chains that do not merge within
 // a span, e.g. long runs of max-length cuts in constant data).  Then it walks
 // the stream's spans in order, re-walking only spans whose entry is stale:
@@ -525,15 +701,15 @@ __global__ __launch_bounds__(kResolveThreads) void serial_kernel(
     const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
     const Candidates cand, const Chains ch, int buf, int slot, uint64_t *stats) {
     __shared__ uint64_t tab[256];
-    __shared__ __attribute__((aligned(16))) uint8_t wins[kResolveThreads * kWin];
     if (ch.changed[slot] == 0) return;
     load_tab1(tab, gear);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * kResolveWaves + (threadIdx.x >> 6);
     if (i >= st.n) return;
-    if (i == 0) stats[3] = 1;
+    if (i == 0 && lane == 0) stats[3] = 1;
     const uint64_t g0 = st.span_base[i], g1 = st.span_base[i + 1];
     if (g1 - g0 < 2) return;
-    Walker w{st, fp, cand, tab, wins + threadIdx.x * kWin, st.ptrs[i], st.lens[i], g0};
+    WaveWalker w{st, fp, cand, tab, st.ptrs[i], st.lens[i], g0, lane};
     uint64_t prev = ch.exit[buf][g0];
     for (uint64_t g = g0 + 1; g < g1; ++g) {
         if (prev == ch.entry[g]) {
@@ -544,13 +720,14 @@ __global__ __launch_bounds__(kResolveThreads) void serial_kernel(
         const uint64_t seg_end = min(off + (1ull << st.span_log2), w.n);
         const int wb = ch.which[g];
         uint32_t cnt;
-        w.cur_sp = ~0ull;
         const uint64_t ex = rewalk(w, prev, seg_end, ch.starts[wb] + g * ch.smax, ch.nstarts[wb][g],
                                    ch.exit[buf][g], ch.starts[1 - wb] + g * ch.smax, cnt);
-        ch.nstarts[1 - wb][g] = cnt;
-        ch.which[g] = (uint8_t)(1 - wb);
-        ch.entry[g] = prev;
-        ch.exit[buf][g] = ex;
+        if (lane == 0) {
+            ch.nstarts[1 - wb][g] = cnt;
+            ch.which[g] = (uint8_t)(1 - wb);
+            ch.entry[g] = prev;
+            ch.exit[buf][g] = ex;
+        }
         prev = ex;
     }
 }
@@ -590,6 +767,8 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sm,
     return r;
 }
 
+// Per span: chunk count -> block-local exclusive prefix (chunk_index) and
+// per-block sums; also the candidate / overflow statistics.
 __global__ __launch_bounds__(kScanBlock) void count_kernel(
     const StreamTable st, const Chains ch, const Candidates cand, const Compact cp) {
     __shared__ uint64_t sm[17];
@@ -602,7 +781,8 @@ __global__ __launch_bounds__(kScanBlock) void count_kernel(
         ov = k > cand.cap;
     }
     uint64_t tot;
-    block_excl_scan(c, sm, tot);
+    const uint64_t ex = block_excl_scan(c, sm, tot);
+    if (g < st.total_spans) cp.chunk_index[g] = ex;
     if (threadIdx.x == 0) cp.block_sums[blockIdx.x] = tot;
     uint64_t tnc, tov;
     block_excl_scan(nc, sm, tnc);
@@ -627,35 +807,32 @@ __global__ __launch_bounds__(kScanBlock) void block_sums_kernel(uint64_t *bs, ui
     if (threadIdx.x == 0) bs[nb] = carry;
 }
 
-__global__ __launch_bounds__(kScanBlock) void write_kernel(
-    const StreamTable st, const Chains ch, int eb, const Compact cp,
-    cdc_chunk_pod *out, uint64_t nb) {
-    __shared__ uint64_t sm[17];
-    const uint64_t g = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x;
-    uint32_t c = 0;
-    int w = 0;
-    if (g < st.total_spans) {
-        w = ch.which[g];
-        c = ch.nstarts[w][g];
+// One wave per span: lane k writes Chunk{offset,length} k of the span
+// (coalesced 16-byte stores), plus first[stream] for a stream's first span and
+// first[n] = total for the last span.  Zero-length streams own no span; the
+// host fills their first[] entries.
+__global__ __launch_bounds__(kResolveThreads) void write_kernel(
+    const StreamTable st, const Chains ch, int eb, const Compact cp, cdc_chunk_pod *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * kResolveWaves + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    const int w = ch.which[g];
+    const uint32_t c = ch.nstarts[w][g];
+    const uint64_t idx = cp.block_sums[g / kScanBlock] + cp.chunk_index[g];
+    const uint64_t *list = ch.starts[w] + g * ch.smax;
+    const uint64_t ex = ch.exit[eb][g];
+    for (uint32_t k = lane; k < c; k += 64) {
+        const uint64_t s = list[k];
+        const uint64_t nx = k + 1 < c ? list[k + 1] : ex;
+        out[idx + k] = cdc_chunk_pod{s, nx - s};
     }
-    uint64_t tot;
-    const uint64_t idx = cp.block_sums[blockIdx.x] + block_excl_scan(c, sm, tot);
-    if (g < st.total_spans) {
-        cp.chunk_index[g] = idx;
-        const uint64_t *list = ch.starts[w] + g * ch.smax;
-        const uint64_t ex = ch.exit[eb][g];
-        for (uint32_t k = 0; k < c; ++k) {
-            const uint64_t s = list[k];
-            const uint64_t nx = k + 1 < c ? list[k + 1] : ex;
-            out[idx + k] = cdc_chunk_pod{s, nx - s};
-        }
+    if (lane == 0) {
+        uint32_t si;
+        uint64_t off;
+        locate(st, g, si, off);
+        if (off == 0) cp.first[si] = idx;
+        if (g + 1 == st.total_spans) cp.first[st.n] = idx + c;
     }
-    if (g == 0) cp.chunk_index[st.total_spans] = cp.block_sums[nb];
-}
-
-__global__ void first_kernel(const StreamTable st, const Compact cp) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= st.n) cp.first[i] = cp.chunk_index[st.span_base[i]];
 }
 
 // FSChunker::chunk_data (fixed_size.rs:32-43): chunk t of the batch.
@@ -711,8 +888,16 @@ hipError_t launch_spec(const StreamTable &st, const FastParams &fp,
                        const uint64_t *d_gear, const Candidates &cand,
                        const Chains &ch, uint64_t *stats, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (unsigned)((st.total_spans + kResolveThreads - 1) / kResolveThreads);
+    const unsigned grid = (unsigned)((st.total_spans + kResolveWaves - 1) / kResolveWaves);
     spec_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, ch, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_trunc(const StreamTable &st, const FastParams &fp,
+                        const uint64_t *d_gear, const Candidates &cand, hipStream_t s) {
+    if (!st.total_spans) return hipSuccess;
+    const unsigned grid = (unsigned)((st.total_spans + kResolveWaves - 1) / kResolveWaves);
+    trunc_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand);
     return hipGetLastError();
 }
 
@@ -720,7 +905,7 @@ hipError_t launch_fixup(const StreamTable &st, const FastParams &fp,
                         const uint64_t *d_gear, const Candidates &cand,
                         const Chains &ch, int iter, uint64_t *stats, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (unsigned)((st.total_spans + kResolveThreads - 1) / kResolveThreads);
+    const unsigned grid = (unsigned)((st.total_spans + kResolveWaves - 1) / kResolveWaves);
     fixup_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, ch, iter, stats);
     return hipGetLastError();
 }
@@ -729,7 +914,7 @@ hipError_t launch_serial(const StreamTable &st, const FastParams &fp,
                          const uint64_t *d_gear, const Candidates &cand,
                          const Chains &ch, int buf, int slot, uint64_t *stats, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (st.n + kResolveThreads - 1) / kResolveThreads;
+    const unsigned grid = (st.n + kResolveWaves - 1) / kResolveWaves;
     serial_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, ch, buf, slot, stats);
     return hipGetLastError();
 }
@@ -738,13 +923,11 @@ hipError_t launch_compact(const StreamTable &st, const Chains &ch, int exit_buf,
                           const Candidates &cand, const Compact &cp,
                           void *d_out, hipStream_t s) {
     const uint64_t nb = (st.total_spans + kScanBlock - 1) / kScanBlock;
-    if (nb) {
-        count_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, ch, cand, cp);
-        block_sums_kernel<<<1, kScanBlock, 0, s>>>(cp.block_sums, nb);
-        write_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(
-            st, ch, exit_buf, cp, reinterpret_cast<cdc_chunk_pod *>(d_out), nb);
-    }
-    first_kernel<<<(st.n + 1 + 255) / 256, 256, 0, s>>>(st, cp);
+    if (!nb) return hipSuccess;
+    count_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, ch, cand, cp);
+    block_sums_kernel<<<1, kScanBlock, 0, s>>>(cp.block_sums, nb);
+    write_kernel<<<(unsigned)((st.total_spans + kResolveWaves - 1) / kResolveWaves), kResolveThreads, 0, s>>>(
+        st, ch, exit_buf, cp, reinterpret_cast<cdc_chunk_pod *>(d_out));
     return hipGetLastError();
 }
 

@@ -49,7 +49,7 @@ struct FastParams {
 struct Candidates {
     uint32_t cap;
     uint32_t *count;  // [spans]: candidates found (> cap = overflowed)
-    uint32_t *pos;    // [spans*cap]: offset in span | bit30 mask_l hit | bit31 mask_s hit
+    uint32_t *pos;    // [spans*cap]: offset in span (bits 0-23) | truncated result (24-29) | bit30 mask_l hit | bit31 mask_s hit
 };
 
 struct Chains {
@@ -72,6 +72,8 @@ struct Compact {
 hipError_t launch_scan(const StreamTable &st, const FastParams &fp,
                        const uint64_t *d_gear, const Candidates &cand,
                        int num_cus, hipStream_t s);
+hipError_t launch_trunc(const StreamTable &st, const FastParams &fp,
+                        const uint64_t *d_gear, const Candidates &cand, hipStream_t s);
 hipError_t launch_spec(const StreamTable &st, const FastParams &fp,
                        const uint64_t *d_gear, const Candidates &cand,
                        const Chains &ch, uint64_t *stats, hipStream_t s);

@@ -191,8 +191,8 @@ int Engine::ensure_host_staging(size_t n) {
     (void)hipHostFree(h_stage_);
     h_stage_ = nullptr;
     const size_t want = n + 64;
-    // ptrs[n] lens[n] span_base[n+1] first[n+1] flag stats[2]
-    HIP_TRY(hipHostMalloc(&h_stage_, (4 * want + 8) * sizeof(uint64_t)));
+    // ptrs[n] lens[n] span_base[n+1] | stats[4] first[n+1] (fixed: first[n+1])
+    HIP_TRY(hipHostMalloc(&h_stage_, (4 * want + 16) * sizeof(uint64_t)));
     h_stage_streams_ = want;
     return CDC_OK;
 }
@@ -215,7 +215,8 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     const size_t o_ns0 = take(S * 4), o_ns1 = take(S * 4), o_which = take(S);
     const size_t o_entry = take(S * 8), o_ex0 = take(S * 8), o_ex1 = take(S * 8);
     const size_t o_changed = take(16), o_ci = take((S + 1) * 8);
-    const size_t o_bs = take((S / 1024 + 2) * 8), o_stats = take(32), o_first = take((N + 1) * 8);
+    // stats[4] and first[N+1] are contiguous: one D2H per batch.
+    const size_t o_bs = take((S / 1024 + 2) * 8), o_stats = take((4 + N + 1) * 8);
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
@@ -243,7 +244,7 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     comp_.chunk_index = reinterpret_cast<uint64_t *>(b + o_ci);
     comp_.block_sums = reinterpret_cast<uint64_t *>(b + o_bs);
     comp_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
-    comp_.first = reinterpret_cast<uint64_t *>(b + o_first);
+    comp_.first = comp_.stats + 4;
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
@@ -335,11 +336,11 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
 int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                      uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_first = h + 3 * h_stage_streams_;
-    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats[4] + changed flags
+    uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1]
     HIP_TRY(hipEventRecord(ev_[0], s));
     HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
+    HIP_TRY(launch_trunc(st, fp_, d_gear_, cand_, s));
     HIP_TRY(launch_spec(st, fp_, d_gear_, cand_, chains_, comp_.stats, s));
     int exit_buf = 0;
     if (st.total_spans > st.n) {  // some stream has >= 2 spans: chains must be joined
@@ -354,11 +355,15 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     }
     HIP_TRY(hipEventRecord(ev_[2], s));
     HIP_TRY(launch_compact(st, chains_, exit_buf, cand_, comp_, d_out, s));
-    HIP_TRY(hipMemcpyAsync(h_first, comp_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h_misc, comp_.stats, 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_misc, comp_.stats, (4 + n + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ev_[3], s));
     HIP_TRY(hipStreamSynchronize(s));
-    std::memcpy(first, h_first, (n + 1) * 8);
+    // Zero-length streams own no span: their first[] is the next stream's.
+    const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
+    uint64_t *hf = h_misc + 4;
+    for (size_t i = n; i-- > 0;)
+        if (lens[i] == 0) hf[i] = hf[i + 1];
+    std::memcpy(first, hf, (n + 1) * 8);
     float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
     HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
     HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
