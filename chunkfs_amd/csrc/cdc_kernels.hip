@@ -25,6 +25,8 @@
 //     exit changes is the exact reference chain ("Resolve").
 //  4. compact kernels: prefix sum of chunk counts and Chunk{offset,length}
 //     output in stream order.
+#include <type_traits>
+
 #include "cdc_kernels.hpp"
 
 namespace cdc {
@@ -34,6 +36,8 @@ constexpr int kScanThreads = 1024;
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kCopies = 32;           // GEAR replicas, one bank pair per lane&31
 constexpr uint32_t kIterBytes = 4096; // 64 lanes x 64 contiguous bytes per wave-iteration
+// 2 blocks of 16 waves per CU = 8 waves/SIMD: caps the scan at 64 VGPRs.
+constexpr int kScanMinWaves = 8;
 constexpr uint32_t kEntCap = 64;      // per-wave LDS list of hitting 16-byte quarters per span
 // Candidate record: offset in span (spans <= 16 MiB) | exact mask hit flags.
 constexpr uint32_t kCandPosMask = 0x00FFFFFFu;
@@ -89,7 +93,7 @@ __device__ __forceinline__ void locate(const StreamTable &st, uint64_t g,
 template <bool kAlign>
 __device__ __forceinline__ uint32_t cand_test(uint64_t h, const FastParams &fp) {
     if constexpr (kAlign) {
-        return __builtin_amdgcn_alignbit((uint32_t)(h >> 32), (uint32_t)h, fp.cm_shift) & fp.cm32;
+        return (uint32_t)(h >> 32) & fp.cm32;  // h pre-shifted by tshift
     } else {
         return ((uint32_t)h & fp.cm_lo) | ((uint32_t)(h >> 32) & fp.cm_hi);
     }
@@ -166,7 +170,7 @@ __device__ __forceinline__ uint4 ld16_guarded(const uint8_t *base, uint32_t p, u
 // quarter) to a per-wave LDS list; exact mask_s/mask_l flags, ordering and the
 // HBM write happen once per span in the flush.
 template <bool kAlign>
-__global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
+__global__ __launch_bounds__(kScanThreads, kScanMinWaves) void scan_kernel(
     const StreamTable st, const FastParams fp,
     const uint64_t *__restrict__ gear, const Candidates cand) {
     __shared__ uint64_t tab[256 * kCopies];  // 64 KiB: entry e, replica c at e*32+c
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
     __shared__ uint32_t ehhi[kScanWaves][kEntCap];
     __shared__ uint32_t ecnt[kScanWaves][kEntCap];
     for (int i = threadIdx.x; i < 256 * kCopies; i += kScanThreads)
-        tab[i] = gear[i / kCopies];
+        tab[i] = gear[i / kCopies] << fp.tshift;  // pre-shifted GEAR (see FastParams)
     __syncthreads();
 
     const char *tabb = reinterpret_cast<const char *>(tab);
@@ -205,38 +209,44 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
 
         uint32_t ne = 0;  // quarter entries appended this span (wave-uniform)
 
-        auto process = [&](const Data64 d, uint32_t pos0, uint32_t qvalid) {
-            const uint64_t P = pass1(tabb, rep1, d);
+        // One wave-iteration over the lane's 64 bytes in d.
+        auto process = [&](const Data64 &d, uint32_t pos0, uint32_t qvalid) {
+            // Pass 1: hash of bytes 16..63 (one chain).
+            uint64_t P = 0;
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) P = shl1_add(P, gear_of(tabb, rep1, word_of(d.q[q], w), b));
+                    if (w & 1) __builtin_amdgcn_sched_barrier(0);  // <= 8 lookups in flight
+                }
+            }
             const uint64_t cin = wave_shr1(P, carry);
             carry = readlane63(P);
             uint64_t h = cin;
-            uint64_t hq[4];
-            uint32_t nq = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                hq[q] = h;
+                const uint64_t h0 = h;  // hash before the quarter (for the flush)
                 uint32_t acc = 0xffffffffu;
 #pragma unroll
-                for (int w = 0; w < 4; ++w)
+                for (int w = 0; w < 4; ++w) {
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         h = shl1_add(h, gear_of(tabb, rep2, word_of(d.q[q], w), b));
                         acc = min(acc, cand_test<kAlign>(h, fp));
                     }
-                nq |= (uint32_t)(acc == 0) << q;
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            nq &= qvalid;
-            if (__ballot(nq != 0)) {  // ~1 hitting quarter per 4 KiB at 12-bit masks
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint64_t m = __ballot((nq >> q) & 1u);
-                    if ((nq >> q) & 1u) {
+                    if (w & 1) __builtin_amdgcn_sched_barrier(0);
+                }
+                const bool hit = acc == 0 && ((qvalid >> q) & 1u);
+                const uint64_t m = __ballot(hit);
+                if (m) {  // ~1 hitting quarter per 4 KiB at 12-bit masks
+                    if (hit) {
                         const uint32_t slot = ne + (uint32_t)__popcll(m & lanemask_lt);
                         if (slot < kEntCap) {
                             epos[wave][slot] = pos0 + 16 * q;
-                            ehlo[wave][slot] = (uint32_t)hq[q];
-                            ehhi[wave][slot] = (uint32_t)(hq[q] >> 32);
+                            ehlo[wave][slot] = (uint32_t)h0;
+                            ehhi[wave][slot] = (uint32_t)(h0 >> 32);
                         }
                     }
                     ne += (uint32_t)__popcll(m);
@@ -294,8 +304,8 @@ __global__ __launch_bounds__(kScanThreads, 2) void scan_kernel(
                     const int j = 4 * w + b;
                     hh = (hh << 1) + gear_of(tabb, rep2, word_of(v, w), b);
                     if (my_pos + j < span_len) {
-                        hs |= (uint32_t)((hh & fp.mask_s) == 0) << j;
-                        hl |= (uint32_t)((hh & fp.mask_l) == 0) << j;
+                        hs |= (uint32_t)((hh & fp.mask_s_sh) == 0) << j;
+                        hl |= (uint32_t)((hh & fp.mask_l_sh) == 0) << j;
                     }
                 }
             ecnt[wave][lane] = __popc(hs | hl);

@@ -39,11 +39,17 @@ struct FastParams {
     uint32_t trunc;          // positions after chunk_start+min whose in-chunk hash differs from the windowed hash
     uint64_t mask_s, mask_l; // Level1 masks
     uint64_t cmask;          // mask_s & mask_l: candidate predicate (superset of both)
-    // Candidate test forms.  align: cmask fits in 32 bits after >> cm_shift, so
-    // the test is one v_alignbit_b32 + one v_and_b32; otherwise lo/hi halves.
+    // Candidate test forms.  Aligned (cm_align): mask_s|mask_l fits in the
+    // 32-bit window [w, w+32), w = ctz(mask_s|mask_l).  The scan then tracks
+    // every hash pre-shifted, h' = h << tshift with tshift = 32 - w (GEAR
+    // pre-shifted the same way), so the window is exactly the high dword of
+    // h' and the test is one v_and_b32 -- no v_alignbit (half rate on gfx950).
+    // General form: unshifted, (lo & cm_lo) | (hi & cm_hi).
     uint32_t cm_align;       // 1 = aligned form usable
-    uint32_t cm_shift, cm32; // aligned form
+    uint32_t tshift;         // scan pre-shift of every hash (0 in the general form)
+    uint32_t cm32;           // aligned: (cmask << tshift) >> 32
     uint32_t cm_lo, cm_hi;   // general form
+    uint64_t mask_s_sh, mask_l_sh;  // mask_s / mask_l << tshift (exact flush tests)
 };
 
 struct Candidates {

@@ -89,12 +89,14 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
             return CDC_EINVAL;
         }
         fp.trunc = top;
-        const uint32_t sh = (uint32_t)__builtin_ctzll(fp.cmask);
-        fp.cm_align = (sh < 32 && (fp.cmask >> sh) <= 0xFFFFFFFFull) ? 1u : 0u;
-        fp.cm_shift = sh < 32 ? sh : 0;
-        fp.cm32 = (uint32_t)(fp.cmask >> fp.cm_shift);
+        const uint32_t wlo = (uint32_t)__builtin_ctzll(all);
+        fp.cm_align = (wlo <= 32 && (all >> wlo) <= 0xFFFFFFFFull) ? 1u : 0u;
+        fp.tshift = fp.cm_align ? 32 - wlo : 0;
+        fp.cm32 = (uint32_t)((fp.cmask << fp.tshift) >> 32);
         fp.cm_lo = (uint32_t)fp.cmask;
         fp.cm_hi = (uint32_t)(fp.cmask >> 32);
+        fp.mask_s_sh = fp.mask_s << fp.tshift;
+        fp.mask_l_sh = fp.mask_l << fp.tshift;
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
         const uint64_t span = 1ull << e->span_log2_;
