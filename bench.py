@@ -9,7 +9,10 @@ Workload at N=1 (BASELINE.json configs[1]): one 1 GiB
 stream of splitmix64(seed=1) bytes, FastCDC min/avg/max = 4/8/16 KiB.  At N>1
 every rank chunks its own 1 GiB stream (seed 1+rank): independent streams,
 no data-path collective, weak scaling.  `--workload batch`
-runs a config-4 shard instead (streams of 64 MiB, seed 1000+i).
+runs config 4 instead: 1024 streams of 64 MiB (stream i: seed 1000+i) split
+into contiguous blocks across the ranks, strong scaling
+(chunkfs_amd/sharding.py).  `host_path` records the PCIe-inclusive rate of
+the host-buffer entry point beside `value` (never as it).
 
 Rank 0 prints ONE JSON line.  `roofline` is for the scan kernel (the only
 HBM-bound kernel): achieved = input bytes per launch / average scan-kernel
@@ -37,7 +40,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", choices=["stream", "batch"], default="stream")
     p.add_argument("--stream-bytes", type=int, default=1 << 30)
-    p.add_argument("--batch-streams", type=int, default=128)
+    p.add_argument("--batch-streams", type=int, default=1024,
+                   help="config 4: total streams, split across ranks (strong scaling)")
     p.add_argument("--batch-stream-bytes", type=int, default=64 << 20)
     p.add_argument("--min", type=int, default=4096)
     p.add_argument("--avg", type=int, default=8192)
@@ -45,6 +49,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline budget (rank 0, N=1 only); 0 disables")
     p.add_argument("--no-parity", action="store_true", help="skip the one-off oracle check")
+    p.add_argument("--no-host-path", action="store_true",
+                   help="skip the one-off host-buffer (PCIe-inclusive) rate")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
     return p.parse_args()
 
@@ -65,16 +71,15 @@ def main():
     torch.cuda.set_device(dev)
 
     import chunkfs_amd as cfa
-    from chunkfs_amd import _lib
+    from chunkfs_amd import _lib, sharding
 
     ch = cfa.FastChunker(cfa.SizeParams(args.min, args.avg, args.max), device=local)
 
     if args.workload == "stream":
-        lens = [args.stream_bytes]
-        seeds = [1 + rank]
+        shard = sharding.stream_shard(rank, world, args.stream_bytes)
     else:
-        lens = [args.batch_stream_bytes] * args.batch_streams
-        seeds = [1000 + rank * args.batch_streams + i for i in range(args.batch_streams)]
+        shard = sharding.batch_shard(rank, world, args.batch_streams, args.batch_stream_bytes)
+    lens, seeds = shard.lens, shard.seeds
     bufs = []
     for n, s in zip(lens, seeds):
         b = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -107,15 +112,11 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed = float(te.item())
+    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, dev)
 
     bytes_rank = sum(lens)
-    total_bytes = bytes_rank * world * args.steps
-    value = total_bytes / elapsed / (1 << 30)
+    total_bytes = sharding.sum_over_ranks(bytes_rank, dev) * args.steps
+    value = sharding.aggregate_gibps(total_bytes, elapsed)
     scan_avg_ms = sum(scan_ms) / len(scan_ms)
     achieved = bytes_rank / (scan_avg_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
     nchunks = int(first[-1])
@@ -128,6 +129,20 @@ def main():
                 traffic = tj.get("hbm_read_bytes_per_launch")
         except Exception:
             traffic = None
+
+    # PCIe-inclusive rate of the host boundary (cdc_chunk_data on a pageable
+    # host buffer: H2D, pipeline, D2H of the chunk list).  Recorded beside
+    # `value`, never as it.
+    host_path = None
+    if rank == 0 and world == 1 and not args.no_host_path:
+        hb = bufs[0].cpu().numpy()
+        ch.chunk_array(hb)  # warm the host-path staging
+        reps, t_h = 3, time.perf_counter()
+        for _ in range(reps):
+            hc = ch.chunk_array(hb)
+        t_h = (time.perf_counter() - t_h) / reps
+        host_path = {"GiBps": hb.size / t_h / (1 << 30), "bytes": int(hb.size), "chunks": int(hc.shape[0]),
+                     "entry": "cdc_chunk_data (pageable host buffer -> H2D -> pipeline -> D2H chunks)"}
 
     parity = None
     cpu_baseline = None
@@ -165,13 +180,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": shard.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)",
             "config": {
                 "workload": ("config2: 1 x 1 GiB stream per GPU" if args.workload == "stream"
-                             else f"config4 shard: {args.batch_streams} x {args.batch_stream_bytes} B streams per GPU"),
+                             else f"config4: {args.batch_streams} x {args.batch_stream_bytes} B streams "
+                                  f"split across {world} GPU(s)"),
                 "algo": "FastCDC v2020 (Level1)", "min": args.min, "avg": args.avg, "max": args.max,
                 "bytes_per_gpu": bytes_rank, "streams_per_gpu": len(lens), "chunks_per_gpu": nchunks,
                 "parallelism": f"independent streams x{world}, no collective",
@@ -182,6 +198,7 @@ def main():
                 "kernel": "scan_kernel (gear candidate scan)", "kernel_ms": scan_avg_ms,
             },
             "cpu_baseline": cpu_baseline,
+            "host_path": host_path,
             "phase_ms": {"scan": scan_avg_ms, "total_device": sum(total_ms) / len(total_ms),
                          "fixup_iterations": max(fix_iters)},
             "parity_vs_oracle": parity,

@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Turn a rocprofv3 FETCH_SIZE pass (tools/pmc.sh) into profiles/<tag>_pmc_traffic.json,
+which bench.py reads for `roofline.traffic`.
+
+FETCH_SIZE is reported in KiB, and on gfx950 it counts exactly half of the
+bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, "HBM [CDNA4]"):
+bytes = FETCH_SIZE * 1024 * 2.
+
+usage: tools/traffic_json.py <fetch counter_collection.csv> <out.json> [workload_bytes]
+"""
+import csv
+import json
+import sys
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    workload = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 30
+    vals, name = [], None
+    for r in csv.DictReader(open(src)):
+        if r["Counter_Name"] == "FETCH_SIZE" and "scan_kernel" in r["Kernel_Name"]:
+            vals.append(float(r["Counter_Value"]))
+            name = r["Kernel_Name"]
+    if not vals:
+        sys.exit("no scan_kernel FETCH_SIZE rows in " + src)
+    per_launch = sum(vals) / len(vals) * 1024 * 2
+    out = {
+        "kernel": "scan_kernel",
+        "kernel_symbol": name,
+        "workload_bytes": workload,
+        "dispatches": len(vals),
+        "fetch_size_kib_mean": sum(vals) / len(vals),
+        "hbm_read_bytes_per_launch": per_launch,
+        "ratio_to_algorithmic": per_launch / workload,
+        "correction": "FETCH_SIZE[KiB] x 1024 x 2 (gfx950 half-count of wide streaming reads)",
+        "source": src,
+    }
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
