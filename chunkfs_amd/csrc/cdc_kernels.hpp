@@ -5,14 +5,13 @@
 //     by the scan kernel (the only HBM-bound kernel).
 //   * spans: every stream is cut into SPAN = 2^span_log2 byte spans; span g of
 //     the batch belongs to stream i with span_base[i] <= g < span_base[i+1].
-//     A span is both the scan unit (one wavefront) and the resolve segment
-//     (one thread).
-//   * candidates: per span, cand_count[g] and up to `cap` records
-//     (cand_pos[g*cap+k] = offset in span, u32; cand_hash[g*cap+k] = windowed
-//     gear hash, bits 0..47 exact), in increasing position order.
-//   * chains: per span two ping-pong lists of chunk starts (starts[b][g*smax+k],
-//     u64 stream offsets), nstarts[b][g], which[g] selects the live one,
-//     entry[g], exit[2][g].
+//     A span is both the scan unit and the resolve unit (one wavefront each).
+//   * candidates: per span, count[g] and up to `cap` u32 records
+//     pos[g*cap+k] (offset in span | truncated result | exact hit flags), in
+//     increasing position order.
+//   * chains: per span the speculative list of chunk starts and, when the
+//     look-back finds it stale, the re-walked one (starts[b][g*smax+k], u64
+//     stream offsets); per-span look-back descriptors (Lookback).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -55,44 +54,35 @@ struct FastParams {
 struct Candidates {
     uint32_t cap;
     uint32_t *count;  // [spans]: candidates found (> cap = overflowed)
-    uint32_t *pos;    // [spans*cap]: offset in span (bits 0-23) | truncated result (24-29) | bit30 mask_l hit | bit31 mask_s hit
+    uint32_t *pos;    // [spans*cap]: offset in span (bits 0-23) | bit30 mask_l hit | bit31 mask_s hit
 };
 
 struct Chains {
     uint32_t smax;
-    uint64_t *starts[2];   // [spans*smax]
-    uint32_t *nstarts[2];  // [spans]
-    uint8_t *which;        // [spans]
-    uint64_t *entry;       // [spans]
-    uint64_t *exit[2];     // [spans]
-    uint32_t *changed;     // [3]: rotating "some exit changed" flags of the Jacobi passes
+    uint64_t *starts[2];   // [spans*smax]: chunk starts of each span (starts[1] unused)
 };
 
-struct Compact {
-    uint64_t *chunk_index;   // [spans+1]
-    uint64_t *block_sums;    // [ceil(spans/1024)+1]
-    uint64_t *stats;         // [4]: candidates, overflow spans, Jacobi passes run, serial used
-    uint64_t *first;         // [n+1]
+// Single-pass resolve state (decoupled look-back over spans, in ticket
+// order).  Reset by the scan kernel of the same batch.
+struct Lookback {
+    uint64_t *desc;     // [waves of 64 spans]: status(62-63) | chunk count (25-61) | exit - span end (0-24)
+    uint64_t *ent;      // [waves]: valid(63) | starts a stream(62) | lane 0's entry - its span start
+    uint32_t *ticket;   // [2]: next span-group ticket, finished groups
+    uint64_t *stats;    // [4] device accumulators: candidates, overflowed spans, re-walked spans, timeouts
+    uint64_t *h_stats;  // host-mapped [4]: copy of stats, written by the last group
+    uint64_t *h_first;  // host-mapped [n+1]: index of each stream's first chunk
 };
 
 hipError_t launch_scan(const StreamTable &st, const FastParams &fp,
                        const uint64_t *d_gear, const Candidates &cand,
-                       int num_cus, hipStream_t s);
-hipError_t launch_trunc(const StreamTable &st, const FastParams &fp,
-                        const uint64_t *d_gear, const Candidates &cand, hipStream_t s);
-hipError_t launch_spec(const StreamTable &st, const FastParams &fp,
-                       const uint64_t *d_gear, const Candidates &cand,
-                       const Chains &ch, uint64_t *stats, hipStream_t s);
-hipError_t launch_fixup(const StreamTable &st, const FastParams &fp,
-                        const uint64_t *d_gear, const Candidates &cand,
-                        const Chains &ch, int iter, uint64_t *stats, hipStream_t s);
-hipError_t launch_serial(const StreamTable &st, const FastParams &fp,
-                         const uint64_t *d_gear, const Candidates &cand,
-                         const Chains &ch, int buf, int slot, uint64_t *stats,
-                         hipStream_t s);
-hipError_t launch_compact(const StreamTable &st, const Chains &ch,
-                          int exit_buf, const Candidates &cand,
-                          const Compact &cp, void *d_out, hipStream_t s);
+                       const Lookback &lb, int num_cus, hipStream_t s);
+hipError_t launch_next(const StreamTable &st, const FastParams &fp,
+                       const uint64_t *d_gear, const Candidates &cand, uint64_t *nxt,
+                       hipStream_t s);
+hipError_t launch_resolve(const StreamTable &st, const FastParams &fp,
+                          const uint64_t *d_gear, const Candidates &cand,
+                          const uint64_t *nxt, const Chains &ch, const Lookback &lb,
+                          void *d_out, hipStream_t s);
 hipError_t launch_fixed(const StreamTable &st, uint64_t chunk_size,
                         const uint64_t *d_first, void *d_out, uint64_t total,
                         hipStream_t s);

@@ -1,11 +1,11 @@
 // engine.cpp -- host orchestration of the gfx950 chunking pipeline.
 //
-// Per batch (DESIGN.md "Pipeline"):
-//   H2D of three tiny per-stream tables -> scan -> spec -> fixup (Jacobi,
-//   until no span exit changes; one flag readback per pass) -> compact ->
-//   D2H of the n+1 per-stream chunk indices.
-// Everything runs on one HIP stream; the candidate lists, chains and output
-// never leave HBM.
+// Per batch (DESIGN.md "Pipeline and kernels"):
+//   H2D of three tiny per-stream tables (skipped when unchanged) -> scan ->
+//   next (record links) -> walk (writes the chunks to HBM and first[n+1] + stats
+//   straight into coherent pinned host memory) -> one stream sync.
+// Everything runs on one HIP stream; candidates, chains and the output never
+// leave HBM.
 #include "engine.hpp"
 
 #include <cmath>
@@ -194,7 +194,7 @@ int Engine::ensure_host_staging(size_t n) {
     h_stage_ = nullptr;
     const size_t want = n + 64;
     // ptrs[n] lens[n] span_base[n+1] | stats[4] first[n+1] (fixed: first[n+1])
-    HIP_TRY(hipHostMalloc(&h_stage_, (4 * want + 16) * sizeof(uint64_t)));
+    HIP_TRY(hipHostMalloc(&h_stage_, (4 * want + 16) * sizeof(uint64_t), hipHostMallocCoherent));
     h_stage_streams_ = want;
     return CDC_OK;
 }
@@ -213,12 +213,9 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
         return o;
     };
     const size_t o_count = take(S * 4), o_pos = take(S * cap * 4);
-    const size_t o_st0 = take(S * smax * 8), o_st1 = take(S * smax * 8);
-    const size_t o_ns0 = take(S * 4), o_ns1 = take(S * 4), o_which = take(S);
-    const size_t o_entry = take(S * 8), o_ex0 = take(S * 8), o_ex1 = take(S * 8);
-    const size_t o_changed = take(16), o_ci = take((S + 1) * 8);
-    // stats[4] and first[N+1] are contiguous: one D2H per batch.
-    const size_t o_bs = take((S / 1024 + 2) * 8), o_stats = take((4 + N + 1) * 8);
+    const size_t o_st0 = take(S * smax * 8), o_nxt = take(S * cap * 8);
+    const size_t o_desc = take(S * 8), o_ent = take(S * 8), o_tk = take(16), o_stats = take(4 * 8);
+    const size_t o_first = take((N + 1) * 8);
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
@@ -235,18 +232,13 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     cand_.pos = reinterpret_cast<uint32_t *>(b + o_pos);
     chains_.smax = (uint32_t)smax;
     chains_.starts[0] = reinterpret_cast<uint64_t *>(b + o_st0);
-    chains_.starts[1] = reinterpret_cast<uint64_t *>(b + o_st1);
-    chains_.nstarts[0] = reinterpret_cast<uint32_t *>(b + o_ns0);
-    chains_.nstarts[1] = reinterpret_cast<uint32_t *>(b + o_ns1);
-    chains_.which = reinterpret_cast<uint8_t *>(b + o_which);
-    chains_.entry = reinterpret_cast<uint64_t *>(b + o_entry);
-    chains_.exit[0] = reinterpret_cast<uint64_t *>(b + o_ex0);
-    chains_.exit[1] = reinterpret_cast<uint64_t *>(b + o_ex1);
-    chains_.changed = reinterpret_cast<uint32_t *>(b + o_changed);
-    comp_.chunk_index = reinterpret_cast<uint64_t *>(b + o_ci);
-    comp_.block_sums = reinterpret_cast<uint64_t *>(b + o_bs);
-    comp_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
-    comp_.first = comp_.stats + 4;
+    chains_.starts[1] = nullptr;
+    d_nxt_ = reinterpret_cast<uint64_t *>(b + o_nxt);
+    lb_.desc = reinterpret_cast<uint64_t *>(b + o_desc);
+    lb_.ent = reinterpret_cast<uint64_t *>(b + o_ent);
+    lb_.ticket = reinterpret_cast<uint32_t *>(b + o_tk);
+    lb_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
+    d_first_ = reinterpret_cast<uint64_t *>(b + o_first);
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
@@ -338,46 +330,40 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
 int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                      uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1]
+    uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1], written by the device
+    Lookback lb = lb_;
+    lb.h_stats = h_misc;
+    lb.h_first = h_misc + 4;
+    h_misc[3] = ~0ull;  // sentinel: overwritten by the resolve kernel's last workgroup
     HIP_TRY(hipEventRecord(ev_[0], s));
-    HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
+    HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, lb, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
-    HIP_TRY(launch_trunc(st, fp_, d_gear_, cand_, s));
-    HIP_TRY(launch_spec(st, fp_, d_gear_, cand_, chains_, comp_.stats, s));
-    int exit_buf = 0;
-    if (st.total_spans > st.n) {  // some stream has >= 2 spans: chains must be joined
-        // kJacobi device passes (each a no-op once converged) and a serial
-        // catch-up that runs only if the last pass still changed an exit: no
-        // host round trip on any path.
-        for (int it = 0; it < kJacobi; ++it)
-            HIP_TRY(launch_fixup(st, fp_, d_gear_, cand_, chains_, it, comp_.stats, s));
-        exit_buf = kJacobi & 1;
-        HIP_TRY(launch_serial(st, fp_, d_gear_, cand_, chains_, exit_buf, (kJacobi - 1) % 3,
-                              comp_.stats, s));
-    }
+    HIP_TRY(launch_next(st, fp_, d_gear_, cand_, d_nxt_, s));
+    HIP_TRY(launch_resolve(st, fp_, d_gear_, cand_, d_nxt_, chains_, lb, d_out, s));
     HIP_TRY(hipEventRecord(ev_[2], s));
-    HIP_TRY(launch_compact(st, chains_, exit_buf, cand_, comp_, d_out, s));
-    HIP_TRY(hipMemcpyAsync(h_misc, comp_.stats, (4 + n + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(ev_[3], s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (h_misc[3] != 0) {
+        set_error(h_misc[3] == ~0ull ? "resolve kernel did not report back"
+                                     : "resolve look-back timed out (internal error)");
+        return CDC_EDEVICE;
+    }
     // Zero-length streams own no span: their first[] is the next stream's.
     const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
     uint64_t *hf = h_misc + 4;
     for (size_t i = n; i-- > 0;)
         if (lens[i] == 0) hf[i] = hf[i + 1];
     std::memcpy(first, hf, (n + 1) * 8);
-    float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+    float t01 = 0, t12 = 0, t02 = 0;
     HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
     HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
-    HIP_TRY(hipEventElapsedTime(&t23, ev_[2], ev_[3]));
-    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
+    HIP_TRY(hipEventElapsedTime(&t02, ev_[0], ev_[2]));
     timing_.scan_ms = t01;
     timing_.resolve_ms = t12;
-    timing_.compact_ms = t23;
-    timing_.total_ms = t03;
+    timing_.compact_ms = 0;  // fused into the resolve kernel
+    timing_.total_ms = t02;
     timing_.candidates = h_misc[0];
     timing_.overflow_spans = (uint32_t)h_misc[1];
-    timing_.fixup_iterations = (uint32_t)h_misc[2] + (h_misc[3] ? 1000u : 0u);
+    timing_.fixup_iterations = (uint32_t)h_misc[2];
     return CDC_OK;
 }
 
@@ -392,8 +378,8 @@ int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
     }
     h_first[n] = t;
     HIP_TRY(hipEventRecord(ev_[0], s));
-    HIP_TRY(hipMemcpyAsync(comp_.first, h_first, (n + 1) * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(launch_fixed(st, min_, comp_.first, d_out, t, s));
+    HIP_TRY(hipMemcpyAsync(d_first_, h_first, (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_fixed(st, min_, d_first_, d_out, t, s));
     HIP_TRY(hipEventRecord(ev_[3], s));
     HIP_TRY(hipStreamSynchronize(s));
     std::memcpy(first, h_first, (n + 1) * 8);

@@ -69,12 +69,16 @@ class Engine {
     size_t ws_streams_ = 0;
     Candidates cand_{};
     Chains chains_{};
-    Compact comp_{};
+    Lookback lb_{};
+    uint64_t *d_nxt_ = nullptr;    // [spans*cap] record links (next_kernel)
+    uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
     const uint8_t **d_ptrs_ = nullptr;
     uint64_t *d_lens_ = nullptr;
     uint64_t *d_span_base_ = nullptr;
 
-    // Pinned host staging for the small per-call tables.
+    // Pinned, device-visible (coherent) host staging: the small per-call
+    // tables going in, stats[4] ++ first[n+1] coming back (written by the
+    // resolve kernel directly, no copy).
     void *h_stage_ = nullptr;
     size_t h_stage_streams_ = 0;
 
@@ -90,8 +94,6 @@ class Engine {
     // they were uploaded into.
     std::vector<uint64_t> tables_;
     uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
-
-    static constexpr int kJacobi = 3;  // device-side Jacobi passes per batch
 };
 
 void set_error(const std::string &msg);

@@ -115,14 +115,15 @@ size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n,
 
 /* Per-phase device time of the last batch (HIP events on the launch
  * stream), milliseconds.  scan = the gear candidate scan kernel (the HBM-bound
- * kernel the roofline is quoted on); resolve = speculative walk + fix-up
- * iterations; compact = scan/write of the output; total = all of it. */
+ * kernel the roofline is quoted on); resolve = truncated-region precompute +
+ * the single-pass resolve (chain walk, look-back, output); compact = 0 (fused
+ * into resolve); total = all of it. */
 typedef struct cdc_timing {
     double scan_ms;
     double resolve_ms;
     double compact_ms;
     double total_ms;
-    uint32_t fixup_iterations;
+    uint32_t fixup_iterations; /* spans whose speculative chain was re-walked */
     uint32_t overflow_spans; /* spans whose candidate list overflowed */
     uint64_t candidates;     /* candidate positions emitted by the scan */
     uint64_t bytes;          /* input bytes of the batch */

@@ -166,6 +166,35 @@ def test_ragged_batch_device():
         assert_same(out[first[i]:first[i + 1]], oracle.fastcdc(a, *sizes), f"stream {i} len={len(a)}")
 
 
+def test_many_streams_cross_wave_boundaries():
+    """150 ragged streams: stream starts fall anywhere inside the walk's
+    64-span waves, and the look-back crosses many stream boundaries."""
+    sizes = SIZES[0]
+    ch = chunker(sizes)
+    rng = np.random.default_rng(77)
+    lens = [int(x) for x in rng.integers(0, 700_000, size=150)]
+    lens[3] = 64 * 65536  # exactly one wave of spans
+    lens[4] = 64 * 65536 + 1
+    arrays = [oracle.splitmix64_bytes(n, 2000 + i) for i, n in enumerate(lens)]
+    out, first = _torch_batch(ch, arrays)
+    for i, a in enumerate(arrays):
+        assert_same(out[first[i]:first[i + 1]], oracle.fastcdc(a, *sizes), f"stream {i} len={len(a)}")
+
+
+def test_mixed_entropy_batch():
+    """Overflowed record lists (low-entropy streams) next to random ones in the
+    same waves: the wave-cooperative fallback runs while other lanes walk."""
+    sizes = SIZES[0]
+    ch = chunker(sizes)
+    arrays = []
+    for i in range(12):
+        pat = ["splitmix64", "const", "periodic", "lowentropy"][i % 4]
+        arrays.append(make_input(pat, 300_000 + 7919 * i, 3000 + i))
+    out, first = _torch_batch(ch, arrays)
+    for i, a in enumerate(arrays):
+        assert_same(out[first[i]:first[i + 1]], oracle.fastcdc(a, *sizes), f"stream {i}")
+
+
 def test_batch_composition_invariance():
     """Determinism: a stream's chunks do not depend on what else is in the batch."""
     sizes = SIZES[0]
