@@ -32,4 +32,6 @@ for k, v in agg.items():
     print(f"{k}: n={len(v)} mean={sum(v)/len(v):.4g} min={min(v):.4g} max={max(v):.4g}")
 PY
 done
+f=$(find $OUT/fetch -name "*counter_collection.csv" | head -1)
+[ -n "$f" ] && python3 tools/traffic_json.py "$f" $OUT/traffic.json 1073741824
 exit 0
