@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline budget (rank 0, N=1 only); 0 disables")
     p.add_argument("--no-parity", action="store_true", help="skip the one-off oracle check")
+    p.add_argument("--no-hash", action="store_true", help="skip the one-off SHA-256 fingerprint rate")
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the one-off host-buffer (PCIe-inclusive) rate")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
@@ -123,6 +124,20 @@ def main():
     achieved = bytes_rank / (scan_avg_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
     nchunks = int(first[-1])
 
+    # SHA-256 of every chunk of stream 0 (device-resident),
+    # reported beside the chunking metric (not part of `value`).
+    fingerprint = None
+    if not args.no_hash and lens and lens[0]:
+        n0 = int(first[1]) - int(first[0])
+        dig = torch.empty((max(n0, 1), 32), dtype=torch.uint8, device=dev)
+        hms = []
+        for _ in range(3):
+            ch.sha256_chunks_device(bufs[0].data_ptr(), out.data_ptr(), n0, dig.data_ptr())
+            hms.append(ch.last_timing()["hash_ms"])
+        hm = sorted(hms)[1]
+        fingerprint = {"algo": "SHA-256 per chunk (Sha256Hasher)", "chunks": n0, "kernel_ms": hm,
+                       "GiBps": lens[0] / (hm * 1e-3) / (1 << 30)}
+
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -145,6 +160,14 @@ def main():
         t_h = (time.perf_counter() - t_h) / reps
         host_path = {"GiBps": hb.size / t_h / (1 << 30), "bytes": int(hb.size), "chunks": int(hc.shape[0]),
                      "entry": "cdc_chunk_data (pageable host buffer -> H2D -> pipeline -> D2H chunks)"}
+        # The reference harness's own path (src/bench/mod.rs:93-140): the
+        # StorageWriter loop over 1 MiB segments, throughput = bytes / summed
+        # chunk_data time (storage.rs:314-316).
+        fs_bytes = min(hb.size, 256 << 20)
+        spans, chunk_s = cfa.write_spans(ch, hb[:fs_bytes])
+        host_path["fs_write_1MiB_segments"] = {
+            "GiBps": fs_bytes / chunk_s / (1 << 30), "bytes": int(fs_bytes), "spans": int(spans.size),
+            "metric": "bytes / summed chunk_data seconds, as CDCFixture::measure"}
 
     parity = None
     cpu_baseline = None
@@ -201,6 +224,7 @@ def main():
             },
             "cpu_baseline": cpu_baseline,
             "host_path": host_path,
+            "fingerprint": fingerprint,
             "phase_ms": {"scan": scan_avg_ms, "total_device": sum(total_ms) / len(total_ms),
                          "resolve": sum(resolve_ms) / len(resolve_ms),
                          "rewalked_spans": max(rewalked)},

@@ -127,6 +127,27 @@ class Chunker:
         assert cnt <= cap
         return out[:cnt]
 
+    def chunk_and_hash(self, data):
+        """chunk_data plus Sha256Hasher::hash (src/hashers.rs:20-36) of every
+        chunk, as StorageWriter::write computes them (storage.rs:324-329).
+        Returns ((n, 2) uint64 chunks, (n, 32) uint8 SHA-256 digests)."""
+        ptr, n, keep = _as_buffer(data)
+        cap = lib().cdc_max_chunk_count(self._h, n)
+        out = np.empty((max(cap, 1), 2), dtype=np.uint64)
+        dig = np.empty((max(cap, 1), 32), dtype=np.uint8)
+        cnt = check(lib().cdc_chunk_and_hash(self._h, ptr, n,
+                                             out.ctypes.data_as(ctypes.POINTER(cdc_chunk_t)),
+                                             dig.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), cap))
+        del keep
+        assert cnt <= cap
+        return out[:cnt], dig[:cnt]
+
+    def sha256_chunks_device(self, d_data, d_chunks, n_chunks, d_digests, stream=None):
+        """SHA-256 of n_chunks chunks of one device-resident stream (device pointers)."""
+        check(lib().cdc_sha256_chunks_device(self._h, ctypes.c_void_p(d_data), ctypes.c_void_p(d_chunks),
+                                             n_chunks, ctypes.c_void_p(d_digests),
+                                             None if stream is None else ctypes.c_void_p(stream)))
+
     def chunk_data(self, data, empty=None):
         """Chunker::chunk_data (src/lib.rs:80): chunks tiling `data`, appended to `empty`."""
         chunks = [] if empty is None else empty

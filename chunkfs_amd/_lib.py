@@ -22,7 +22,8 @@ EXPORTS = [
     "cdc_create", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
     "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear",
     "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
-    "cdc_fs_write", "cdc_fill_splitmix64_device", "cdc_version",
+    "cdc_fs_write", "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
+    "cdc_fill_splitmix64_device", "cdc_version",
 ]
 
 
@@ -46,6 +47,7 @@ class cdc_timing_t(ctypes.Structure):
         ("overflow_spans", ctypes.c_uint32),
         ("candidates", ctypes.c_uint64),
         ("bytes", ctypes.c_uint64),
+        ("hash_ms", ctypes.c_double),
     ]
 
 
@@ -102,6 +104,10 @@ def lib():
     L.cdc_last_timing.restype = ctypes.c_int
     L.cdc_fs_write.argtypes = [P, P, sz, sz, u64p, sz, ctypes.POINTER(ctypes.c_double)]
     L.cdc_fs_write.restype = ctypes.c_int64
+    L.cdc_sha256_chunks_device.argtypes = [P, P, P, sz, P, P]
+    L.cdc_sha256_chunks_device.restype = ctypes.c_int
+    L.cdc_chunk_and_hash.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), u8p, sz]
+    L.cdc_chunk_and_hash.restype = ctypes.c_int64
     L.cdc_fill_splitmix64_device.argtypes = [P, sz, ctypes.c_uint64, P]
     L.cdc_fill_splitmix64_device.restype = ctypes.c_int
     L.cdc_version.argtypes = []

@@ -101,6 +101,24 @@ int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
     return n;
 }
 
+int cdc_sha256_chunks_device(cdc_handle_t *h, const uint8_t *d_data,
+                             const cdc_chunk_t *d_chunks, size_t n_chunks,
+                             uint8_t *d_digests, void *hip_stream) {
+    if (!h) return (int)bad_handle();
+    return h->engine->sha256_device(d_data, d_chunks, n_chunks, d_digests,
+                                    static_cast<hipStream_t>(hip_stream));
+}
+
+int64_t cdc_chunk_and_hash(cdc_handle_t *h, const uint8_t *data, size_t len,
+                           cdc_chunk_t *out, uint8_t *digests, size_t cap) {
+    if (!h) return bad_handle();
+    if (cap && !digests) {
+        cdc::set_error("cdc_chunk_and_hash: digests is NULL");
+        return CDC_EINVAL;
+    }
+    return h->engine->chunk_host(data, len, out, cap, digests);
+}
+
 int cdc_fill_splitmix64_device(uint8_t *d_buf, size_t len, uint64_t seed, void *hip_stream) {
     if (len && !d_buf) {
         cdc::set_error("NULL buffer");

@@ -13,6 +13,7 @@
 #include <cstring>
 
 #include "../../include/chunkfs_amd_tables.h"
+#include "sha256.hpp"
 
 namespace cdc {
 
@@ -150,6 +151,7 @@ int Engine::init() {
     HIP_TRY(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking));
     for (auto &ev : ev_) HIP_TRY(hipEventCreate(&ev));
     HIP_TRY(hipMalloc(&d_gear_, 256 * sizeof(uint64_t)));
+    HIP_TRY(hipMalloc(&d_counter_, sizeof(unsigned long long)));
     HIP_TRY(hipMemcpy(d_gear_, CHUNKFS_AMD_GEAR, 256 * sizeof(uint64_t), hipMemcpyHostToDevice));
     return CDC_OK;
 }
@@ -161,6 +163,8 @@ Engine::~Engine() {
     (void)hipFree(d_gear_);
     (void)hipFree(d_data_);
     (void)hipFree(d_out_);
+    (void)hipFree(d_dig_);
+    (void)hipFree(d_counter_);
     (void)hipHostFree(h_stage_);
     for (auto &ev : ev_)
         if (ev) (void)hipEventDestroy(ev);
@@ -259,7 +263,9 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     }
     HIP_TRY(hipSetDevice(device_));
     hipStream_t s = stream ? stream : own_stream_;
+    const double hash_ms = timing_.hash_ms;  // (reported with the batch it hashed)
     timing_ = cdc_timing_t{};
+    timing_.hash_ms = hash_ms;
     uint64_t bytes = 0, need = 0;
     for (size_t i = 0; i < n; ++i) {
         bytes += lens[i];
@@ -391,7 +397,7 @@ int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
 }
 
 int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out,
-                           size_t cap) {
+                           size_t cap, uint8_t *digests) {
     if (len && !data) {
         set_error("cdc_chunk_data: data is NULL");
         return CDC_EINVAL;
@@ -426,11 +432,42 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out,
     const int64_t count = chunk_batch_device(1, &p, &l, d_out_, d_out_cap_, first, own_stream_);
     if (count < 0) return count;
     const size_t copy = (size_t)count < cap ? (size_t)count : cap;
+    if (digests && copy) {
+        if (d_dig_cap_ < (size_t)count) {
+            (void)hipFree(d_dig_);
+            d_dig_ = nullptr;
+            d_dig_cap_ = 0;
+            const size_t want = (size_t)count + (size_t)count / 8 + 64;
+            HIP_TRY(hipMalloc(&d_dig_, want * 32));
+            d_dig_cap_ = want;
+        }
+        const int rc = sha256_device(d_data_, d_out_, (size_t)count, d_dig_, own_stream_);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(digests, d_dig_, copy * 32, hipMemcpyDeviceToHost, own_stream_));
+    }
     if (copy) {
         HIP_TRY(hipMemcpyAsync(out, d_out_, copy * sizeof(cdc_chunk_t), hipMemcpyDeviceToHost, own_stream_));
         HIP_TRY(hipStreamSynchronize(own_stream_));
     }
     return count;
+}
+
+int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
+                          uint8_t *d_digests, hipStream_t s) {
+    if (n && (!d_data || !d_chunks || !d_digests)) {
+        set_error("cdc_sha256_chunks_device: NULL argument");
+        return CDC_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    hipStream_t st = s ? s : own_stream_;
+    HIP_TRY(hipEventRecord(ev_[3], st));
+    HIP_TRY(launch_sha256(d_data, d_chunks, n, d_digests, d_counter_, num_cus_, st));
+    HIP_TRY(hipEventRecord(ev_[2], st));
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ev_[3], ev_[2]));
+    timing_.hash_ms = ms;
+    return CDC_OK;
 }
 
 int Engine::fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s) {

@@ -22,7 +22,13 @@ class Engine {
                       int device, Engine **out);
     ~Engine();
 
-    int64_t chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, size_t cap);
+    // chunk_data on a host buffer; with `digests` (32 B per chunk, cap
+    // entries) also the SHA-256 of every chunk (StorageWriter's hashing).
+    int64_t chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, size_t cap,
+                       uint8_t *digests = nullptr);
+    // SHA-256 of chunks of one device-resident stream (Sha256Hasher::hash).
+    int sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
+                      uint8_t *d_digests, hipStream_t s);
     int64_t chunk_batch_device(size_t n, const uint8_t *const *d_streams,
                                const uint64_t *lens, cdc_chunk_t *d_out,
                                size_t out_cap, uint64_t *first, hipStream_t stream);
@@ -87,6 +93,9 @@ class Engine {
     size_t d_data_bytes_ = 0;
     cdc_chunk_t *d_out_ = nullptr;
     size_t d_out_cap_ = 0;
+    uint8_t *d_dig_ = nullptr;               // [d_dig_cap_ * 32] digests (host path)
+    size_t d_dig_cap_ = 0;
+    unsigned long long *d_counter_ = nullptr;  // SHA-256 work counter
 
     cdc_timing_t timing_{};
 

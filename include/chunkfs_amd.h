@@ -127,6 +127,7 @@ typedef struct cdc_timing {
     uint32_t overflow_spans; /* spans whose candidate list overflowed */
     uint64_t candidates;     /* candidate positions emitted by the scan */
     uint64_t bytes;          /* input bytes of the batch */
+    double hash_ms;          /* last cdc_sha256_chunks_device / cdc_chunk_and_hash kernel time */
 } cdc_timing_t;
 
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t);
@@ -141,6 +142,20 @@ int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t);
 int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
                      size_t seg_size, uint64_t *span_lengths, size_t cap,
                      double *chunk_seconds);
+
+/* ---- Chunk fingerprints -------------------------------
+ * Sha256Hasher::hash (src/hashers.rs:20-36), applied to every chunk as
+ * StorageWriter::write does (storage.rs:324-329).  DEVICE arrays:
+ * d_digests[32*i .. 32*i+32) = SHA-256(d_data[d_chunks[i].offset .. +length)).
+ * Synchronises hip_stream (NULL = the handle's stream) before returning. */
+int cdc_sha256_chunks_device(cdc_handle_t *h, const uint8_t *d_data,
+                             const cdc_chunk_t *d_chunks, size_t n_chunks,
+                             uint8_t *d_digests, void *hip_stream);
+
+/* chunk_data + SHA-256 of each chunk on a HOST buffer: as cdc_chunk_data, and
+ * digests[32*i ..] for the first min(count, cap) chunks. */
+int64_t cdc_chunk_and_hash(cdc_handle_t *h, const uint8_t *data, size_t len,
+                           cdc_chunk_t *out, uint8_t *digests, size_t cap);
 
 /* ---- Synthetic data -----------------------------------------
  * Fill a DEVICE buffer with the splitmix64 stream: little-endian u64 words,
