@@ -20,6 +20,7 @@ import ctypes
 
 import numpy as np
 
+from . import _lib
 from ._lib import ALGO, CdcError, cdc_chunk_t, cdc_timing_t, check, lib
 
 KB = 1024
@@ -256,6 +257,42 @@ def write_spans(chunker, data, seg_size=SEG_SIZE):
     del keep
     assert cnt <= cap
     return out[:cnt], secs.value
+
+
+class DedupIndex:
+    """The reference's chunk Database keyed by SHA-256 digest (database.rs:74-87,
+    first insert wins) with its storage statistics (storage.rs:193-240), as a
+    device hash set on one GPU."""
+
+    def __init__(self, capacity, device=0):
+        h = ctypes.c_void_p()
+        check(lib().cdc_index_create(device, capacity, ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().cdc_index_destroy(h)
+            self._h = None
+
+    def insert_device(self, d_digests, d_chunks, n, d_new=None, stream=None):
+        """Database::insert of n (digest, chunk) pairs (device pointers), in chunk
+        order.  Returns the number of new digests; d_new (optional u8[n]) marks them."""
+        return check(lib().cdc_index_insert_device(
+            self._h, ctypes.c_void_p(d_digests), ctypes.c_void_p(d_chunks), n,
+            None if d_new is None else ctypes.c_void_p(d_new),
+            None if stream is None else ctypes.c_void_p(stream)))
+
+    def clear(self):
+        check(lib().cdc_index_clear(self._h))
+
+    def stats(self):
+        s = _lib.cdc_index_stats_t()
+        check(lib().cdc_index_stats(self._h, ctypes.byref(s)))
+        d = {f: getattr(s, f) for f, _ in _lib.cdc_index_stats_t._fields_}
+        d["cdc_dedup_ratio"] = d["bytes_written"] / d["unique_bytes"] if d["unique_bytes"] else float("nan")
+        d["average_chunk_size"] = d["unique_bytes"] // d["unique_chunks"] if d["unique_chunks"] else 0
+        return d
 
 
 def version():

@@ -23,6 +23,8 @@ EXPORTS = [
     "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear",
     "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
     "cdc_fs_write", "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
+    "cdc_index_create", "cdc_index_destroy", "cdc_index_clear", "cdc_index_insert_device",
+    "cdc_index_stats",
     "cdc_fill_splitmix64_device", "cdc_version",
 ]
 
@@ -35,6 +37,11 @@ class CdcError(RuntimeError):
 
 class cdc_chunk_t(ctypes.Structure):
     _fields_ = [("offset", ctypes.c_uint64), ("length", ctypes.c_uint64)]
+
+
+class cdc_index_stats_t(ctypes.Structure):
+    _fields_ = [("chunks_written", ctypes.c_uint64), ("bytes_written", ctypes.c_uint64),
+                ("unique_chunks", ctypes.c_uint64), ("unique_bytes", ctypes.c_uint64)]
 
 
 class cdc_timing_t(ctypes.Structure):
@@ -108,6 +115,16 @@ def lib():
     L.cdc_sha256_chunks_device.restype = ctypes.c_int
     L.cdc_chunk_and_hash.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), u8p, sz]
     L.cdc_chunk_and_hash.restype = ctypes.c_int64
+    L.cdc_index_create.argtypes = [ctypes.c_int, sz, ctypes.POINTER(P)]
+    L.cdc_index_create.restype = ctypes.c_int
+    L.cdc_index_destroy.argtypes = [P]
+    L.cdc_index_destroy.restype = None
+    L.cdc_index_clear.argtypes = [P]
+    L.cdc_index_clear.restype = ctypes.c_int
+    L.cdc_index_insert_device.argtypes = [P, P, P, sz, P, P]
+    L.cdc_index_insert_device.restype = ctypes.c_int64
+    L.cdc_index_stats.argtypes = [P, ctypes.POINTER(cdc_index_stats_t)]
+    L.cdc_index_stats.restype = ctypes.c_int
     L.cdc_fill_splitmix64_device.argtypes = [P, sz, ctypes.c_uint64, P]
     L.cdc_fill_splitmix64_device.restype = ctypes.c_int
     L.cdc_version.argtypes = []

@@ -157,6 +157,36 @@ int cdc_sha256_chunks_device(cdc_handle_t *h, const uint8_t *d_data,
 int64_t cdc_chunk_and_hash(cdc_handle_t *h, const uint8_t *data, size_t len,
                            cdc_chunk_t *out, uint8_t *digests, size_t cap);
 
+/* ---- Dedup index --------------------------------------
+ * The chunk Database of the reference keyed by SHA-256 digest
+ * (src/system/database.rs:74-87: HashMap, `entry(key).or_insert`, i.e. the
+ * FIRST insert of a digest wins) and the storage statistics built on it
+ * (src/system/storage.rs:193-240), as a device hash set. */
+typedef struct cdc_index cdc_index_t;
+
+typedef struct cdc_index_stats {
+    uint64_t chunks_written;  /* chunks inserted so far */
+    uint64_t bytes_written;   /* size_written: bytes of all inserted chunks */
+    uint64_t unique_chunks;   /* distinct digests */
+    uint64_t unique_bytes;    /* total_cdc_size: bytes of the first chunk of each digest */
+} cdc_index_stats_t;
+/* cdc_dedup_ratio = bytes_written / unique_bytes (storage.rs:203-205);
+ * average_chunk_size = unique_bytes / unique_chunks (storage.rs:208-220). */
+
+/* Index on `device` for up to `capacity` distinct digests. */
+int cdc_index_create(int device, size_t capacity, cdc_index_t **out);
+void cdc_index_destroy(cdc_index_t *ix);
+/* Database::clear + size_written = 0 (storage.rs:236-240). */
+int cdc_index_clear(cdc_index_t *ix);
+/* Database::insert of n (digest, chunk) pairs in chunk order (DEVICE arrays:
+ * 32-byte digests, cdc_chunk_t records).  d_new (nullable, DEVICE u8[n])
+ * receives 1 where the chunk's digest was not in the index before it.
+ * Returns the number of new digests (CDC_ENOMEM past capacity). */
+int64_t cdc_index_insert_device(cdc_index_t *ix, const uint8_t *d_digests,
+                                const cdc_chunk_t *d_chunks, size_t n,
+                                uint8_t *d_new, void *hip_stream);
+int cdc_index_stats(const cdc_index_t *ix, cdc_index_stats_t *out);
+
 /* ---- Synthetic data -----------------------------------------
  * Fill a DEVICE buffer with the splitmix64 stream: little-endian u64 words,
  * word i = mix64(seed + (i+1) * 0x9E3779B97F4A7C15). */
