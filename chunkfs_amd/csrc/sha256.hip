@@ -118,7 +118,15 @@ __global__ __launch_bounds__(kShaThreads) void sha256_kernel(const uint8_t *__re
                 uint32_t d[17];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) d[i] = src[i];
-                d[16] = sh ? src[16] : 0u;
+                d[16] = 0;
+                if (sh) {  // the block's last bytes; never read past the chunk
+                    if (al + 68 <= start + len) {
+                        d[16] = src[16];
+                    } else {
+                        g_u8 *b = (g_u8 *)(data + al + 64);
+                        for (uint32_t j = 0; j < sh; ++j) d[16] |= (uint32_t)b[j] << (8 * j);
+                    }
+                }
                 const uint32_t sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
