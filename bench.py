@@ -49,7 +49,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline budget (rank 0, N=1 only); 0 disables")
     p.add_argument("--no-parity", action="store_true", help="skip the one-off oracle check")
-    p.add_argument("--no-hash", action="store_true", help="skip the one-off SHA-256 fingerprint rate")
+    p.add_argument("--hash", action="store_true", help="also report the SHA-256 fingerprint rate (§8f row 2)")
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the one-off host-buffer (PCIe-inclusive) rate")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
@@ -127,7 +127,7 @@ def main():
     # SHA-256 of every chunk of stream 0 (device-resident),
     # reported beside the chunking metric (not part of `value`).
     fingerprint = None
-    if not args.no_hash and lens and lens[0]:
+    if args.hash and lens and lens[0]:
         n0 = int(first[1]) - int(first[0])
         dig = torch.empty((max(n0, 1), 32), dtype=torch.uint8, device=dev)
         hms = []
@@ -216,6 +216,7 @@ def main():
                 "algo": "FastCDC v2020 (Level1)", "min": args.min, "avg": args.avg, "max": args.max,
                 "bytes_per_gpu": bytes_rank, "streams_per_gpu": len(lens), "chunks_per_gpu": nchunks,
                 "parallelism": f"independent streams x{world}, no collective",
+                "pipeline": int(os.environ.get("CHUNKFS_AMD_PIPELINE", "1")),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -10,6 +10,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/chunkfs_amd_tables.h"
@@ -66,6 +67,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
     e->avg_ = avg;
     e->max_ = max;
     e->device_ = device;
+    if (const char *pv = std::getenv("CHUNKFS_AMD_PIPELINE")) e->pipeline_ = std::atoi(pv) == 2 ? 2 : 1;
     if (algo == CDC_ALGO_FASTCDC) {
         if (min < kMinimumMin || min > kMinimumMax || avg < kAverageMin ||
             avg > kAverageMax || max < kMaximumMin || max > kMaximumMax) {
@@ -220,6 +222,11 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     const size_t o_st0 = take(S * smax * 8), o_nxt = take(S * cap * 8);
     const size_t o_desc = take(S * 8), o_ent = take(S * 8), o_tk = take(16), o_stats = take(4 * 8);
     const size_t o_first = take((N + 1) * 8);
+    // pipeline 1 state
+    const size_t o1_st1 = take(S * smax * 8), o1_ns0 = take(S * 4), o1_ns1 = take(S * 4);
+    const size_t o1_which = take(S), o1_entry = take(S * 8), o1_ex0 = take(S * 8), o1_ex1 = take(S * 8);
+    const size_t o1_changed = take(16), o1_ci = take((S + 1) * 8), o1_bs = take((S / 1024 + 2) * 8);
+    const size_t o1_stats = take((4 + N + 1) * 8);  // stats[4] ++ first[N+1]: one D2H
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
@@ -243,6 +250,20 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     lb_.ticket = reinterpret_cast<uint32_t *>(b + o_tk);
     lb_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
     d_first_ = reinterpret_cast<uint64_t *>(b + o_first);
+    chains1_.smax = (uint32_t)smax;
+    chains1_.starts[0] = chains_.starts[0];
+    chains1_.starts[1] = reinterpret_cast<uint64_t *>(b + o1_st1);
+    chains1_.nstarts[0] = reinterpret_cast<uint32_t *>(b + o1_ns0);
+    chains1_.nstarts[1] = reinterpret_cast<uint32_t *>(b + o1_ns1);
+    chains1_.which = reinterpret_cast<uint8_t *>(b + o1_which);
+    chains1_.entry = reinterpret_cast<uint64_t *>(b + o1_entry);
+    chains1_.exit[0] = reinterpret_cast<uint64_t *>(b + o1_ex0);
+    chains1_.exit[1] = reinterpret_cast<uint64_t *>(b + o1_ex1);
+    chains1_.changed = reinterpret_cast<uint32_t *>(b + o1_changed);
+    comp1_.chunk_index = reinterpret_cast<uint64_t *>(b + o1_ci);
+    comp1_.block_sums = reinterpret_cast<uint64_t *>(b + o1_bs);
+    comp1_.stats = reinterpret_cast<uint64_t *>(b + o1_stats);
+    comp1_.first = comp1_.stats + 4;
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
@@ -333,8 +354,55 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     return (int64_t)first[n];
 }
 
+int Engine::run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+                        uint64_t *first, hipStream_t s) {
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1]
+    HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(v1::launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
+    HIP_TRY(hipEventRecord(ev_[1], s));
+    HIP_TRY(v1::launch_trunc(st, fp_, d_gear_, cand_, s));
+    HIP_TRY(v1::launch_spec(st, fp_, d_gear_, cand_, chains1_, comp1_.stats, s));
+    int exit_buf = 0;
+    if (st.total_spans > st.n) {  // some stream has >= 2 spans: chains must be joined
+        // kJacobi device passes (each a no-op once converged) and a serial
+        // catch-up that runs only if the last pass still changed an exit: no
+        // host round trip on any path.
+        for (int it = 0; it < v1::kJacobi; ++it)
+            HIP_TRY(v1::launch_fixup(st, fp_, d_gear_, cand_, chains1_, it, comp1_.stats, s));
+        exit_buf = v1::kJacobi & 1;
+        HIP_TRY(v1::launch_serial(st, fp_, d_gear_, cand_, chains1_, exit_buf, (v1::kJacobi - 1) % 3,
+                                  comp1_.stats, s));
+    }
+    HIP_TRY(hipEventRecord(ev_[2], s));
+    HIP_TRY(v1::launch_compact(st, chains1_, exit_buf, cand_, comp1_, d_out, s));
+    HIP_TRY(hipMemcpyAsync(h_misc, comp1_.stats, (4 + n + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ev_[3], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // Zero-length streams own no span: their first[] is the next stream's.
+    const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
+    uint64_t *hf = h_misc + 4;
+    for (size_t i = n; i-- > 0;)
+        if (lens[i] == 0) hf[i] = hf[i + 1];
+    std::memcpy(first, hf, (n + 1) * 8);
+    float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
+    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
+    HIP_TRY(hipEventElapsedTime(&t23, ev_[2], ev_[3]));
+    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
+    timing_.scan_ms = t01;
+    timing_.resolve_ms = t12;
+    timing_.compact_ms = t23;
+    timing_.total_ms = t03;
+    timing_.candidates = h_misc[0];
+    timing_.overflow_spans = (uint32_t)h_misc[1];
+    timing_.fixup_iterations = (uint32_t)h_misc[2] + (h_misc[3] ? 1000u : 0u);
+    return CDC_OK;
+}
+
 int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                      uint64_t *first, hipStream_t s) {
+    if (pipeline_ == 1) return run_fast_v1(st, d_out, n, first, s);
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1], written by the device
     Lookback lb = lb_;

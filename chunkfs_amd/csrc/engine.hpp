@@ -12,6 +12,7 @@
 
 #include "../../include/chunkfs_amd.h"
 #include "cdc_kernels.hpp"
+#include "pipeline_v1.hpp"
 
 namespace cdc {
 
@@ -52,6 +53,8 @@ class Engine {
     int ensure_host_staging(size_t n);
     int run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                  uint64_t *first, hipStream_t s);
+    int run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+                    uint64_t *first, hipStream_t s);
     int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                   cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
 
@@ -60,6 +63,10 @@ class Engine {
     int device_ = 0;
     int num_cus_ = 256;
     FastParams fp_{};
+    // FastCDC pipeline: 1 = pipeline_v1.hip (GPU-validated, default), 2 =
+    // cdc_kernels.hip (per-lane sub-span scan, record links + lane walk);
+    // environment CHUNKFS_AMD_PIPELINE at cdc_create.
+    int pipeline_ = 1;
     uint32_t span_log2_ = 16;
     uint32_t cap_ = 0, smax_ = 0;
     std::string describe_;
@@ -76,6 +83,8 @@ class Engine {
     Candidates cand_{};
     Chains chains_{};
     Lookback lb_{};
+    v1::Chains chains1_{};         // pipeline 1 (pipeline_v1.hip)
+    v1::Compact comp1_{};
     uint64_t *d_nxt_ = nullptr;    // [spans*cap] record links (next_kernel)
     uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
     const uint8_t **d_ptrs_ = nullptr;

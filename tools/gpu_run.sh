@@ -17,7 +17,7 @@ timeout -k 10 400 python bench.py --steps $STEPS --warmup 3 > $OUT/bench_$TAG.js
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench_$TAG.json; tail -5 $OUT/bench_$TAG.err
 [ $rc -eq 0 ] || exit $rc
 
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --no-host-path --no-hash > $OUT/prof_$TAG.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --no-host-path > $OUT/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -3 $OUT/prof_$TAG.log
 find $OUT/prof_$TAG -name "*kernel_stats.csv" | head -3
 exit $rc

@@ -9,7 +9,7 @@ rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 run() {  # name, counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "scan_kernel" --output-format csv \
-      -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity --no-host-path --no-hash \
+      -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity --no-host-path \
       > $OUT/$name.log 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
