@@ -27,6 +27,8 @@ EXPORTS = [
     "cdc_index_stats",
     "cdc_fill_splitmix64_device", "cdc_version",
 ]
+# include/chunkfs_amd_debug.h (diagnostics, not part of the drop-in boundary)
+DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy"]
 
 
 class CdcError(RuntimeError):
@@ -127,6 +129,12 @@ def lib():
     L.cdc_index_stats.restype = ctypes.c_int
     L.cdc_fill_splitmix64_device.argtypes = [P, sz, ctypes.c_uint64, P]
     L.cdc_fill_splitmix64_device.restype = ctypes.c_int
+    L.cdc_debug_pipeline.argtypes = [P]
+    L.cdc_debug_pipeline.restype = ctypes.c_int
+    L.cdc_debug_record_cap.argtypes = [P]
+    L.cdc_debug_record_cap.restype = ctypes.c_uint32
+    L.cdc_debug_copy.argtypes = [P, ctypes.c_int, P, sz]
+    L.cdc_debug_copy.restype = ctypes.c_int64
     L.cdc_version.argtypes = []
     L.cdc_version.restype = ctypes.c_char_p
     del u8p

@@ -35,6 +35,7 @@ def build(force=False):
     common = [os.path.join(CSRC, h) for h in HEADERS] + [
         os.path.join(ROOT, "include", "chunkfs_amd.h"),
         os.path.join(ROOT, "include", "chunkfs_amd_tables.h"),
+        os.path.join(ROOT, "include", "chunkfs_amd_debug.h"),
     ]
     objs = []
     for src in SOURCES:

@@ -3,6 +3,7 @@
 #include <vector>
 
 #include "../../include/chunkfs_amd.h"
+#include "../../include/chunkfs_amd_debug.h"
 #include "engine.hpp"
 #include "storage_writer.hpp"
 
@@ -132,6 +133,19 @@ int cdc_fill_splitmix64_device(uint8_t *d_buf, size_t len, uint64_t seed, void *
         return CDC_EDEVICE;
     }
     return CDC_OK;
+}
+
+int cdc_debug_pipeline(const cdc_handle_t *h) { return h ? h->engine->pipeline() : (int)bad_handle(); }
+
+uint32_t cdc_debug_record_cap(const cdc_handle_t *h) { return h ? h->engine->record_cap() : 0; }
+
+int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes) {
+    if (!h) return bad_handle();
+    if (max_bytes && !out) {
+        cdc::set_error("cdc_debug_copy: out is NULL");
+        return CDC_EINVAL;
+    }
+    return h->engine->debug_copy(what, out, max_bytes);
 }
 
 const char *cdc_version(void) { return "chunkfs_amd 0.1 gfx950 abi 1"; }

@@ -348,6 +348,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     st.n = (uint32_t)n;
     st.span_log2 = sl2;
     st.total_spans = spans;
+    last_spans_ = algo_ == CDC_ALGO_FASTCDC ? spans : 0;
     rc = algo_ == CDC_ALGO_FASTCDC ? run_fast(st, d_out, n, first, s)
                                    : run_fixed(st, n, lens, d_out, first, s);
     if (rc) return rc;
@@ -536,6 +537,33 @@ int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, si
     HIP_TRY(hipEventElapsedTime(&ms, ev_[3], ev_[2]));
     timing_.hash_ms = ms;
     return CDC_OK;
+}
+
+int64_t Engine::debug_copy(int what, void *out, size_t max_bytes) {
+    if (algo_ != CDC_ALGO_FASTCDC || !ws_) {
+        set_error("debug_copy: no FastCDC batch yet");
+        return CDC_EINVAL;
+    }
+    const void *src = nullptr;
+    size_t bytes = 0;
+    if (what == 0) {
+        src = cand_.count;
+        bytes = last_spans_ * 4;
+    } else if (what == 1) {
+        src = cand_.pos;
+        bytes = last_spans_ * cap_ * 4;
+    } else if (what == 2) {
+        src = d_nxt_;
+        bytes = last_spans_ * cap_ * 8;
+    } else {
+        set_error("debug_copy: unknown array");
+        return CDC_EINVAL;
+    }
+    if (bytes > max_bytes) bytes = max_bytes;
+    HIP_TRY(hipSetDevice(device_));
+    HIP_TRY(hipStreamSynchronize(own_stream_));
+    if (bytes) HIP_TRY(hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost));
+    return (int64_t)bytes;
 }
 
 int Engine::fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s) {

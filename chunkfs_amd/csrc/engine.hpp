@@ -45,6 +45,13 @@ class Engine {
     cdc_algo_t algo() const { return algo_; }
     int device() const { return device_; }
     int fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s);
+    // Debug (include/chunkfs_amd_debug.h): copy an intermediate array of the
+    // last FastCDC batch to the host.  what: 0 = per-span candidate counts
+    // (u32), 1 = candidate records (u32, cap per span), 2 = record links of
+    // pipeline 2 (u64, cap per span).  Returns bytes copied.
+    int64_t debug_copy(int what, void *out, size_t max_bytes);
+    uint32_t record_cap() const { return cap_; }
+    int pipeline() const { return pipeline_; }
 
   private:
     Engine() = default;
@@ -112,6 +119,7 @@ class Engine {
     // they were uploaded into.
     std::vector<uint64_t> tables_;
     uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
+    uint64_t last_spans_ = 0;  // spans of the last FastCDC batch (debug_copy)
 };
 
 void set_error(const std::string &msg);

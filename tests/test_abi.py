@@ -12,10 +12,11 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "chunkfs_amd.h")
+DEBUG_HEADER = os.path.join(ROOT, "include", "chunkfs_amd_debug.h")
 
 
-def _declared():
-    txt = open(HEADER).read()
+def _declared(path=HEADER):
+    txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(cdc_[a-z0-9_]+)\s*\(", txt)))
 
@@ -31,6 +32,10 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert name in exported, name
         assert hasattr(L, name)
+    debug = _declared(DEBUG_HEADER)
+    assert sorted(_lib.DEBUG_EXPORTS) == debug
+    for name in debug:
+        assert name in exported, name
 
 
 def test_version_string():
