@@ -736,7 +736,7 @@ __device__ void walk_lanes(const StreamTable &st, const FastParams &fp, const Ca
 __global__ __launch_bounds__(kResolveThreads) void walk_kernel(
     const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear,
     const Candidates cand, const uint64_t *__restrict__ nxt, const Chains ch,
-    const Lookback lb, cdc_chunk_pod *out) {
+    const Lookback lb, cdc_chunk_pod *out, uint64_t out_cap) {
     __shared__ uint64_t tab[256];
     __shared__ uint32_t win[kResolveThreads * 13];
     __shared__ uint32_t grp;
@@ -869,10 +869,14 @@ __global__ __launch_bounds__(kResolveThreads) void walk_kernel(
             const uint64_t base = before + excl;
             if (L.act) {
                 const uint32_t c = cnt;
-                for (uint32_t k = 0; k < c; ++k) {
-                    const uint64_t c0 = list[k];
-                    const uint64_t nx = k + 1 < c ? list[k + 1] : exit;
-                    out[base + k] = cdc_chunk_pod{c0, nx - c0};
+                if (base + c > out_cap || c > ch.smax) {
+                    n_to = 1;  // impossible for a correct chain: report, never write out of bounds
+                } else {
+                    for (uint32_t k = 0; k < c; ++k) {
+                        const uint64_t c0 = list[k];
+                        const uint64_t nx = k + 1 < c ? list[k + 1] : exit;
+                        out[base + k] = cdc_chunk_pod{c0, nx - c0};
+                    }
                 }
                 if (L.first) lb.h_first[L.si] = base;
                 if (g + 1 == st.total_spans) lb.h_first[st.n] = base + c;
@@ -968,12 +972,12 @@ hipError_t launch_next(const StreamTable &st, const FastParams &fp,
 hipError_t launch_resolve(const StreamTable &st, const FastParams &fp,
                           const uint64_t *d_gear, const Candidates &cand,
                           const uint64_t *nxt, const Chains &ch, const Lookback &lb,
-                          void *d_out, hipStream_t s) {
+                          void *d_out, uint64_t out_cap, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
     const uint64_t nwaves = (st.total_spans + 63) / 64;
     const unsigned grid = (unsigned)((nwaves + kResolveWaves - 1) / kResolveWaves);
     walk_kernel<<<grid, kResolveThreads, 0, s>>>(st, fp, d_gear, cand, nxt, ch, lb,
-                                                 reinterpret_cast<cdc_chunk_pod *>(d_out));
+                                                 reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap);
     return hipGetLastError();
 }
 

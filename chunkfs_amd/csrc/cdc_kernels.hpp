@@ -82,7 +82,7 @@ hipError_t launch_next(const StreamTable &st, const FastParams &fp,
 hipError_t launch_resolve(const StreamTable &st, const FastParams &fp,
                           const uint64_t *d_gear, const Candidates &cand,
                           const uint64_t *nxt, const Chains &ch, const Lookback &lb,
-                          void *d_out, hipStream_t s);
+                          void *d_out, uint64_t out_cap, hipStream_t s);
 hipError_t launch_fixed(const StreamTable &st, uint64_t chunk_size,
                         const uint64_t *d_first, void *d_out, uint64_t total,
                         hipStream_t s);

@@ -301,6 +301,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
         }
     }
     timing_.bytes = bytes;
+    out_cap_ = out_cap;
     if (need > out_cap) {
         set_error("out_cap < cdc_batch_max_chunks()");
         return CDC_EINVAL;
@@ -414,12 +415,12 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, lb, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
     HIP_TRY(launch_next(st, fp_, d_gear_, cand_, d_nxt_, s));
-    HIP_TRY(launch_resolve(st, fp_, d_gear_, cand_, d_nxt_, chains_, lb, d_out, s));
+    HIP_TRY(launch_resolve(st, fp_, d_gear_, cand_, d_nxt_, chains_, lb, d_out, out_cap_, s));
     HIP_TRY(hipEventRecord(ev_[2], s));
     HIP_TRY(hipStreamSynchronize(s));
     if (h_misc[3] != 0) {
         set_error(h_misc[3] == ~0ull ? "resolve kernel did not report back"
-                                     : "resolve look-back timed out (internal error)");
+                                     : "resolve look-back timed out or chain overflowed (internal error)");
         return CDC_EDEVICE;
     }
     // Zero-length streams own no span: their first[] is the next stream's.
