@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--max", type=int, default=16384)
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline budget (rank 0, N=1 only); 0 disables")
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="also time the oracle on this many host threads (one stream each); 0 disables")
     p.add_argument("--no-parity", action="store_true", help="skip the one-off oracle check")
     p.add_argument("--hash", action="store_true", help="also report the SHA-256 fingerprint rate (§8f row 2)")
     p.add_argument("--no-host-path", action="store_true",
@@ -194,6 +196,14 @@ def main():
                 "sample": f"{passes} whole-buffer pass(es) over stream 0 ({host[0].size} B) of this workload; "
                           "oracle/cdc_oracle.c scalar C restatement of fastcdc v2020 (gcc -O3), single thread",
             }
+            if args.cpu_threads > 1:
+                thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+                nb, wall = oracle.time_fastcdc_threads(host[0], args.min, args.avg, args.max, thr,
+                                                       args.cpu_seconds / 2)
+                cpu_baseline["multi_thread"] = {
+                    "value": nb / wall / (1 << 30), "unit": "GiB/s", "cores": thr,
+                    "sample": f"{thr} threads, each chunking its own {host[0].size // thr} B slice of stream 0 "
+                              f"as an independent stream for ~{args.cpu_seconds / 2:.0f} s"}
 
     if rank == 0:
         line = {

@@ -116,6 +116,35 @@ def fs_write(algo, data, mn, avg=0, mx=0, seg_size=1 << 20, gear=None):
     return out[:cnt], secs.value
 
 
+def time_fastcdc_threads(data, mn, avg, mx, threads, seconds):
+    """Aggregate CPU rate with `threads` workers, each chunking its own slice of
+    `data` as an independent stream (one thread per stream on
+    the host cores).  The C oracle runs without the GIL (ctypes).  Returns
+    (bytes processed, wall seconds)."""
+    import threading
+    import time as _t
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    per = data.size // threads
+    slices = [data[i * per:(i + 1) * per] for i in range(threads)]
+    done = [0] * threads
+    stop = _t.perf_counter() + seconds
+
+    def work(i):
+        while True:
+            time_fastcdc(slices[i], mn, avg, mx)
+            done[i] += slices[i].size
+            if _t.perf_counter() >= stop:
+                return
+
+    t0 = _t.perf_counter()
+    ws = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join()
+    return sum(done), _t.perf_counter() - t0
+
+
 def time_fastcdc(data, mn, avg, mx):
     data = np.ascontiguousarray(data, dtype=np.uint8)
     c = ctypes.c_int64()

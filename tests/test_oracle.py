@@ -135,3 +135,10 @@ def test_splitmix64_generator_definition():
     words = [mix((seed + (i + 1) * 0x9E3779B97F4A7C15) & M) for i in range(5)]
     exp = b"".join(w.to_bytes(8, "little") for w in words)[:37]
     assert oracle.splitmix64_bytes(37, seed).tobytes() == exp
+
+
+def test_threaded_cpu_baseline_helper():
+    """bench.py's multi-thread CPU baseline: workers chunk disjoint slices."""
+    data = oracle.splitmix64_bytes(8 << 20, 3)
+    nb, wall = oracle.time_fastcdc_threads(data, 4096, 8192, 16384, threads=4, seconds=0.2)
+    assert nb >= data.size and nb % (data.size // 4) == 0 and wall > 0
