@@ -1,22 +1,28 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident FastCDC throughput on MI355X (BASELINE.json metric).
 
-A "step" = one full pass of the chunking hot path (scan -> resolve -> compact,
-final Chunk{offset,length} list in HBM) over the rank's synthetic input, which
-is already resident in HBM when the timed region starts.
+A "step" = one full pass of the chunking hot path (candidate scan -> chain
+resolve -> Chunk{offset,length} list in HBM) over the rank's synthetic input,
+which is already resident in HBM when the timed region starts.
 
-Workload at N=1 (BASELINE.json configs[1]): one 1 GiB
-stream of splitmix64(seed=1) bytes, FastCDC min/avg/max = 4/8/16 KiB.  At N>1
-every rank chunks its own 1 GiB stream (seed 1+rank): independent streams,
-no data-path collective, weak scaling.  `--workload batch`
-runs config 4 instead: 1024 streams of 64 MiB (stream i: seed 1000+i) split
-into contiguous blocks across the ranks, strong scaling
-(chunkfs_amd/sharding.py).  `host_path` records the PCIe-inclusive rate of
-the host-buffer entry point beside `value` (never as it).
+Workloads:
+  * N = 1 (default `--workload stream`): BASELINE configs[1] / config 2 --
+    one 1 GiB stream of splitmix64(seed=1) bytes, FastCDC 4/8/16 KiB.
+  * N > 1 (default `--workload batch`): config 4 -- 1024 independent 64 MiB
+    streams (stream i: seed 1000+i) split into contiguous blocks across the
+    ranks, strong scaling, no data-path collective (chunkfs_amd/sharding.py).
+    `--workload stream` at N > 1 gives every rank its own 1 GiB stream (weak).
+
+Launch: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
+environment starts `torch.distributed.run` with N ranks as a CHILD process
+(this process never touches the GPU) and exits with its status.  Under an
+external launcher WORLD_SIZE must equal --gpus.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the scan kernel (the only
 HBM-bound kernel): achieved = input bytes per launch / average scan-kernel
-duration measured with HIP events around that launch on its own stream.
+duration measured with HIP events around that launch on the engine's stream.
+`roofline.traffic` comes from a PMC file under profiles/ only when that
+file's recorded source digest equals this build's (chunkfs_amd.build).
 `cpu_baseline` times the oracle's scalar C restatement (oracle/cdc_oracle.c)
 on a bounded sample on this host, rank 0 at N=1 only.
 """
@@ -24,21 +30,25 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, HBM section)
+METRIC = "GiB/s chunked device-resident, FastCDC 4/8/16 KiB avg, at 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["stream", "batch"], default="stream")
+    p.add_argument("--workload", choices=["stream", "batch"], default=None,
+                   help="default: stream at N=1, batch (config 4) at N>1")
     p.add_argument("--stream-bytes", type=int, default=1 << 30)
     p.add_argument("--batch-streams", type=int, default=1024,
                    help="config 4: total streams, split across ranks (strong scaling)")
@@ -48,199 +58,385 @@ def parse():
     p.add_argument("--max", type=int, default=16384)
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="bounded CPU-baseline budget (rank 0, N=1 only); 0 disables")
-    p.add_argument("--cpu-threads", type=int, default=16,
-                   help="also time the oracle on this many host threads (one stream each); 0 disables")
+    p.add_argument("--cpu-threads", type=int, default=-1,
+                   help="threads for the multi-thread CPU leg (-1: every usable host core, 0: off)")
     p.add_argument("--no-parity", action="store_true", help="skip the one-off oracle check")
+    p.add_argument("--no-sweep", action="store_true",
+                   help="skip the avg 4/16 KiB and low-entropy lines (N=1)")
     p.add_argument("--hash", action="store_true", help="also report the SHA-256 fingerprint rate (§8f row 2)")
     p.add_argument("--no-host-path", action="store_true",
-                   help="skip the one-off host-buffer (PCIe-inclusive) rate")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
-    return p.parse_args()
+                   help="skip the one-off host-buffer (PCIe-inclusive) rates")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU launcher test only
+    a = p.parse_args(argv)
+    if a.workload is None:
+        a.workload = "stream" if a.gpus == 1 else "batch"
+    return a
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+# Launcher
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """Start args.gpus ranks under torch.distributed.run as a child process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------
+# Engines: the HIP engine, and a CPU stub (fixed-size cuts in numpy) that lets
+# tests/test_bench_launcher.py exercise the launcher and the reductions with
+# gloo on a machine without a GPU.  The stub is never a product path.
+
+class DeviceEngine:
+    def __init__(self, args, local):
+        import torch
+        import chunkfs_amd as cfa
+        from chunkfs_amd import _lib
+        self.torch, self.cfa, self._lib = torch, cfa, _lib
+        self.dev = torch.device("cuda", local)
+        self.local = local
+        self.ch = cfa.FastChunker(cfa.SizeParams(args.min, args.avg, args.max), device=local)
+
+    def fill(self, lens, seeds):
+        torch = self.torch
+        self.bufs = []
+        for n, s in zip(lens, seeds):
+            b = torch.empty(max(n, 16), dtype=torch.uint8, device=self.dev)
+            self._lib.check(self._lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, s, None))
+            self.bufs.append(b)
+        self.lens = list(lens)
+        self.ptrs = [b.data_ptr() for b in self.bufs]
+        self.cap = self.ch.batch_max_chunks(self.lens)
+        self.out = torch.empty((max(self.cap, 1), 2), dtype=torch.int64, device=self.dev)
+        torch.cuda.synchronize()
+
+    def step(self):
+        return self.ch.chunk_batch_device(self.ptrs, self.lens, self.out.data_ptr(), self.cap)
+
+    def timing(self):
+        return self.ch.last_timing()
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+
+class StubEngine:
+    def __init__(self, args, local):
+        import torch
+        self.torch = torch
+        self.dev = torch.device("cpu")
+        self.cs = args.avg
+
+    def fill(self, lens, seeds):
+        self.lens = list(lens)
+
+    def step(self):
+        first = [0]
+        for n in self.lens:
+            first.append(first[-1] + -(-n // self.cs))
+        return first
+
+    def timing(self):
+        return {"scan_ms": 0.0, "total_ms": 0.0, "resolve_ms": 0.0, "fixup_iterations": 0}
+
+    def sync(self):
+        pass
+
+
+# ---------------------------------------------------------------------------
+# Host facts for the CPU baseline
+
+def host_facts():
+    facts = {"nproc": os.cpu_count()}
+    try:
+        facts["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        facts["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    facts["cgroup_cpu_quota"] = quota
+    try:
+        for ln in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if ln.startswith("Model name:"):
+                facts["cpu_model"] = ln.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    usable = facts["affinity"] or 1
+    if quota:
+        usable = max(1, min(usable, int(quota)))
+    facts["usable_cores"] = usable
+    return facts
+
+
+def cpu_baseline_leg(args, host0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    secs, passes, done = 0.0, 0, 0
+    while passes == 0 or secs < args.cpu_seconds:
+        t, _ = oracle.time_fastcdc(host0, args.min, args.avg, args.max)
+        secs += t
+        passes += 1
+        done += host0.size
+    facts = host_facts()
+    out = {
+        "value": done / secs / (1 << 30), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"{passes} whole-buffer pass(es) over stream 0 ({host0.size} B) of this workload; "
+                  "oracle/cdc_oracle.c scalar C restatement of fastcdc v2020 (gcc -O3), single thread",
+        "host": facts,
+    }
+    thr = facts["usable_cores"] if args.cpu_threads < 0 else args.cpu_threads
+    if thr > 1:
+        nb, wall = oracle.time_fastcdc_threads(host0, args.min, args.avg, args.max, thr, args.cpu_seconds / 2)
+        out["multi_thread"] = {
+            "value": nb / wall / (1 << 30), "unit": "GiB/s", "cores": thr,
+            "sample": f"{thr} threads (every usable host core), each chunking its own "
+                      f"{host0.size // thr} B slice of stream 0 as an independent stream for "
+                      f"~{args.cpu_seconds / 2:.0f} s"}
+    return out
+
+
+def traffic_for_build(path, bytes_rank):
+    """HBM bytes per scan launch from a PMC JSON of THIS build (same source
+    digest and workload), else None."""
+    if not os.path.exists(path):
+        return None, None
+    try:
+        from chunkfs_amd import build as b
+        tj = json.load(open(path))
+        if tj.get("workload_bytes") == bytes_rank and tj.get("source_digest") == b.source_digest():
+            return tj.get("hbm_read_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def sweep_lines(args, eng, steps):
+    """Extra single-GPU lines: avg 4 KiB and 16 KiB (min = avg/2, max = 2*avg)
+    on the same 1 GiB stream, and 1 GiB of low-entropy data (zeros; a 61-byte
+    period) at 4/8/16 KiB, each with an oracle parity check after timing."""
+    import numpy as np
+    import torch
+    import chunkfs_amd as cfa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n = eng.lens[0]
+    base = eng.bufs[0]
+    period = torch.from_numpy(oracle.splitmix64_bytes(61, 7)).to(eng.dev)
+    inputs = {
+        "splitmix64": base,
+        "zeros": torch.zeros(n, dtype=torch.uint8, device=eng.dev),
+        "periodic61": period.repeat(-(-n // 61))[:n].contiguous(),
+    }
+    cases = [("avg4k", (2048, 4096, 8192), "splitmix64"), ("avg16k", (8192, 16384, 32768), "splitmix64"),
+             ("zeros", (4096, 8192, 16384), "zeros"), ("periodic61", (4096, 8192, 16384), "periodic61")]
+    res = {}
+    for name, sizes, inp in cases:
+        buf = inputs[inp]
+        ch = cfa.FastChunker(cfa.SizeParams(*sizes), device=eng.local)
+        cap = ch.batch_max_chunks([n])
+        out = torch.empty((cap, 2), dtype=torch.int64, device=eng.dev)
+        for _ in range(2):
+            first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+        torch.cuda.synchronize()
+        scan, tot = [], []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+            t = ch.last_timing()
+            scan.append(t["scan_ms"])
+            tot.append(t["total_ms"])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        got = out[:int(first[1])].cpu().numpy().view(np.uint64)
+        parity = None
+        if not args.no_parity:
+            ref = oracle.fastcdc(buf.cpu().numpy(), *sizes)
+            parity = bool(got.shape == ref.shape and (got == ref).all())
+        res[name] = {"sizes": list(sizes), "data": inp, "GiBps": n * steps / el / (1 << 30),
+                     "ms_per_step": el / steps * 1e3, "scan_ms": sum(scan) / len(scan),
+                     "device_total_ms": sum(tot) / len(tot), "chunks": int(first[1]), "parity_vs_oracle": parity}
+        ch.close()
+        del out
+    return res
+
+
+def host_path_leg(eng):
+    """PCIe-inclusive rates of the host boundary, recorded beside `value`,
+    never as it: cdc_chunk_data on a 1 GiB host buffer, and the
+    reference harness's own measure -- the StorageWriter loop over 1 MiB
+    segments, bytes / summed chunk_data seconds (src/bench/mod.rs:93-140,
+    src/system/storage.rs:314-316)."""
+    import chunkfs_amd as cfa
+    hb = eng.bufs[0][:eng.lens[0]].cpu().numpy()
+    ch = eng.ch
+    ch.chunk_array(hb)
+    reps, t_h = 3, time.perf_counter()
+    for _ in range(reps):
+        hc = ch.chunk_array(hb)
+    t_h = (time.perf_counter() - t_h) / reps
+    hp = {"GiBps": hb.size / t_h / (1 << 30), "bytes": int(hb.size), "chunks": int(hc.shape[0]),
+          "entry": "cdc_chunk_data (pageable host buffer -> H2D -> pipeline -> D2H chunks)"}
+    fs_bytes = min(hb.size, 256 << 20)
+    spans, chunk_s = cfa.write_spans(ch, hb[:fs_bytes])
+    hp["fs_write_1MiB_segments"] = {
+        "GiBps": fs_bytes / chunk_s / (1 << 30), "bytes": int(fs_bytes), "spans": int(spans.size),
+        "metric": "bytes / summed chunk_data seconds, as CDCFixture::measure"}
+    return hp
+
+
+# ---------------------------------------------------------------------------
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
     import numpy as np
     import torch
     import torch.distributed as dist
+    from chunkfs_amd import sharding
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if args.stub:
+        eng = StubEngine(args, local)
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    import chunkfs_amd as cfa
-    from chunkfs_amd import _lib, sharding
-
-    ch = cfa.FastChunker(cfa.SizeParams(args.min, args.avg, args.max), device=local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        eng = DeviceEngine(args, local)
+    dev = eng.dev
 
     if args.workload == "stream":
         shard = sharding.stream_shard(rank, world, args.stream_bytes)
     else:
         shard = sharding.batch_shard(rank, world, args.batch_streams, args.batch_stream_bytes)
-    lens, seeds = shard.lens, shard.seeds
-    bufs = []
-    for n, s in zip(lens, seeds):
-        b = torch.empty(n, dtype=torch.uint8, device=dev)
-        _lib.check(_lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, s, None))
-        bufs.append(b)
-    ptrs = [b.data_ptr() for b in bufs]
-    cap = ch.batch_max_chunks(lens)
-    out = torch.empty((cap, 2), dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
-
-    def step():
-        return ch.chunk_batch_device(ptrs, lens, out.data_ptr(), cap)
+    eng.fill(shard.lens, shard.seeds)
 
     for _ in range(args.warmup):
-        first = step()
+        first = eng.step()
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    scan_ms = []
-    total_ms = []
-    rewalked = []
-    resolve_ms = []
+    eng.sync()
+    scan_ms, total_ms, resolve_ms, rewalked = [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        first = step()
-        t = ch.last_timing()
+        first = eng.step()
+        t = eng.timing()
         scan_ms.append(t["scan_ms"])
         total_ms.append(t["total_ms"])
-        rewalked.append(t["fixup_iterations"])  # spans whose speculative chain was re-walked
         resolve_ms.append(t["resolve_ms"])
-    torch.cuda.synchronize()
+        rewalked.append(t["fixup_iterations"])
+    eng.sync()
     if world > 1:
         dist.barrier()
     elapsed = sharding.max_over_ranks(time.perf_counter() - t0, dev)
 
-    bytes_rank = sum(lens)
+    bytes_rank = sum(shard.lens)
     total_bytes = sharding.sum_over_ranks(bytes_rank, dev) * args.steps
     value = sharding.aggregate_gibps(total_bytes, elapsed)
     scan_avg_ms = sum(scan_ms) / len(scan_ms)
-    achieved = bytes_rank / (scan_avg_ms * 1e-3) / 1e9  # GB/s, algorithmic bytes of one launch
     nchunks = int(first[-1])
+    total_chunks = sharding.sum_over_ranks(nchunks, dev)
+    ms_per_step = elapsed / args.steps * 1e3
+    achieved = bytes_rank / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else None
+    e2e = bytes_rank / (ms_per_step * 1e-3) / 1e9  # per-GPU bytes / wall step time
 
-    # SHA-256 of every chunk of stream 0 (device-resident),
-    # reported beside the chunking metric (not part of `value`).
-    fingerprint = None
-    if args.hash and lens and lens[0]:
-        n0 = int(first[1]) - int(first[0])
-        dig = torch.empty((max(n0, 1), 32), dtype=torch.uint8, device=dev)
-        hms = []
-        for _ in range(3):
-            ch.sha256_chunks_device(bufs[0].data_ptr(), out.data_ptr(), n0, dig.data_ptr())
-            hms.append(ch.last_timing()["hash_ms"])
-        hm = sorted(hms)[1]
-        fingerprint = {"algo": "SHA-256 per chunk (Sha256Hasher)", "chunks": n0, "kernel_ms": hm,
-                       "GiBps": lens[0] / (hm * 1e-3) / (1 << 30)}
-
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("workload_bytes") == bytes_rank and tj.get("kernel", "").startswith("scan_kernel"):
-                traffic = tj.get("hbm_read_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    # PCIe-inclusive rate of the host boundary (cdc_chunk_data on a pageable
-    # host buffer: H2D, pipeline, D2H of the chunk list).  Recorded beside
-    # `value`, never as it.
-    host_path = None
-    if rank == 0 and world == 1 and not args.no_host_path:
-        hb = bufs[0].cpu().numpy()
-        ch.chunk_array(hb)  # warm the host-path staging
-        reps, t_h = 3, time.perf_counter()
-        for _ in range(reps):
-            hc = ch.chunk_array(hb)
-        t_h = (time.perf_counter() - t_h) / reps
-        host_path = {"GiBps": hb.size / t_h / (1 << 30), "bytes": int(hb.size), "chunks": int(hc.shape[0]),
-                     "entry": "cdc_chunk_data (pageable host buffer -> H2D -> pipeline -> D2H chunks)"}
-        # The reference harness's own path (src/bench/mod.rs:93-140): the
-        # StorageWriter loop over 1 MiB segments, throughput = bytes / summed
-        # chunk_data time (storage.rs:314-316).
-        fs_bytes = min(hb.size, 256 << 20)
-        spans, chunk_s = cfa.write_spans(ch, hb[:fs_bytes])
-        host_path["fs_write_1MiB_segments"] = {
-            "GiBps": fs_bytes / chunk_s / (1 << 30), "bytes": int(fs_bytes), "spans": int(spans.size),
-            "metric": "bytes / summed chunk_data seconds, as CDCFixture::measure"}
-
-    parity = None
-    cpu_baseline = None
-    if rank == 0 and world == 1 and (not args.no_parity or args.cpu_seconds > 0):
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        host = [b.cpu().numpy() for b in bufs[:1]]
+    extras = {}
+    if rank == 0 and world == 1 and not args.stub:
+        if args.hash and shard.lens[0]:
+            n0 = int(first[1]) - int(first[0])
+            dig = torch.empty((max(n0, 1), 32), dtype=torch.uint8, device=dev)
+            hms = []
+            for _ in range(3):
+                eng.ch.sha256_chunks_device(eng.bufs[0].data_ptr(), eng.out.data_ptr(), n0, dig.data_ptr())
+                hms.append(eng.ch.last_timing()["hash_ms"])
+            hm = sorted(hms)[1]
+            extras["fingerprint"] = {"algo": "SHA-256 per chunk (Sha256Hasher)", "chunks": n0, "kernel_ms": hm,
+                                     "GiBps": shard.lens[0] / (hm * 1e-3) / (1 << 30)}
+        if not args.no_host_path:
+            extras["host_path"] = host_path_leg(eng)
         if not args.no_parity:
-            got = out[:int(first[1])].cpu().numpy().view(np.uint64)
-            ref = oracle.fastcdc(host[0], args.min, args.avg, args.max)
-            parity = bool(got.shape == ref.shape and (got == ref).all())
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            checked = []
+            for i in range(min(len(shard.lens), 4)):
+                got = eng.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
+                ref = oracle.fastcdc(eng.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
+                checked.append(bool(got.shape == ref.shape and (got == ref).all()))
+            extras["parity_vs_oracle"] = all(checked)
+            extras["parity_streams_checked"] = len(checked)
+        if not args.no_sweep and args.workload == "stream":
+            extras["sweep"] = sweep_lines(args, eng, max(5, args.steps // 2))
         if args.cpu_seconds > 0:
-            secs, passes, done = 0.0, 0, 0
-            while passes == 0 or secs < args.cpu_seconds:
-                t, _ = oracle.time_fastcdc(host[0], args.min, args.avg, args.max)
-                secs += t
-                passes += 1
-                done += host[0].size
-            cpu_baseline = {
-                "value": done / secs / (1 << 30),
-                "unit": "GiB/s",
-                "cores": 1,
-                "kind": "port",
-                "sample": f"{passes} whole-buffer pass(es) over stream 0 ({host[0].size} B) of this workload; "
-                          "oracle/cdc_oracle.c scalar C restatement of fastcdc v2020 (gcc -O3), single thread",
-            }
-            if args.cpu_threads > 1:
-                thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-                nb, wall = oracle.time_fastcdc_threads(host[0], args.min, args.avg, args.max, thr,
-                                                       args.cpu_seconds / 2)
-                cpu_baseline["multi_thread"] = {
-                    "value": nb / wall / (1 << 30), "unit": "GiB/s", "cores": thr,
-                    "sample": f"{thr} threads, each chunking its own {host[0].size // thr} B slice of stream 0 "
-                              f"as an independent stream for ~{args.cpu_seconds / 2:.0f} s"}
+            extras["cpu_baseline"] = cpu_baseline_leg(args, eng.bufs[0][:shard.lens[0]].cpu().numpy())
 
+    traffic, traffic_src = traffic_for_build(args.traffic_json, bytes_rank)
     if rank == 0:
         line = {
-            "metric": "GiB/s chunked device-resident, FastCDC 4/8/16 KiB avg, at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": value,
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": shard.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes generated on device)",
             "config": {
-                "workload": ("config2: 1 x 1 GiB stream per GPU" if args.workload == "stream"
+                "workload": ("config2: 1 x %d B stream per GPU" % args.stream_bytes if args.workload == "stream"
                              else f"config4: {args.batch_streams} x {args.batch_stream_bytes} B streams "
                                   f"split across {world} GPU(s)"),
                 "algo": "FastCDC v2020 (Level1)", "min": args.min, "avg": args.avg, "max": args.max,
-                "bytes_per_gpu": bytes_rank, "streams_per_gpu": len(lens), "chunks_per_gpu": nchunks,
+                "bytes_per_gpu": bytes_rank, "streams_per_gpu": len(shard.lens), "chunks_total": total_chunks,
                 "parallelism": f"independent streams x{world}, no collective",
-                "pipeline": int(os.environ.get("CHUNKFS_AMD_PIPELINE", "1")),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "scan_kernel (gear candidate scan)", "kernel_ms": scan_avg_ms,
+                "algorithmic_bytes_per_launch": bytes_rank,
+                "end_to_end": {"achieved": e2e, "frac": e2e / HBM_PEAK_GBS,
+                               "definition": "per-GPU input bytes / wall ms_per_step"},
             },
-            "cpu_baseline": cpu_baseline,
-            "host_path": host_path,
-            "fingerprint": fingerprint,
+            "cpu_baseline": extras.pop("cpu_baseline", None),
             "phase_ms": {"scan": scan_avg_ms, "total_device": sum(total_ms) / len(total_ms),
-                         "resolve": sum(resolve_ms) / len(resolve_ms),
-                         "rewalked_spans": max(rewalked)},
-            "parity_vs_oracle": parity,
+                         "resolve": sum(resolve_ms) / len(resolve_ms), "rewalked_spans": max(rewalked)},
         }
+        line.update(extras)
+        if args.stub:
+            line["data"] = "stub engine (CPU launcher test; not a measurement)"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -173,14 +173,17 @@ class Chunker:
 
     # -- device-resident batch (configs 2, 4) --------------------------------
     def chunk_batch_device(self, d_ptrs, lens, d_out_ptr, out_cap, stream=0):
-        """Chunk n streams already in HBM.  Returns the host array first[n+1]."""
-        n = len(lens)
-        ptrs = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(int(p)) for p in d_ptrs])
-        lens_a = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in lens])
-        first = (ctypes.c_uint64 * (n + 1))()
-        check(lib().cdc_chunk_batch_device(self._h, n, ptrs, lens_a, ctypes.c_void_p(int(d_out_ptr)),
-                                           out_cap, first, ctypes.c_void_p(int(stream))))
-        return np.frombuffer(first, dtype=np.uint64).copy()
+        """Chunk n streams already in HBM.  Returns the host array first[n+1].
+        `d_ptrs` / `lens` may be uint64 numpy arrays (no per-call conversion)."""
+        ptrs = np.ascontiguousarray(np.asarray(d_ptrs, dtype=np.uint64))
+        lens_a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        n = int(lens_a.size)
+        first = np.empty(n + 1, dtype=np.uint64)
+        check(lib().cdc_chunk_batch_device(self._h, n, ctypes.c_void_p(ptrs.ctypes.data),
+                                           ctypes.c_void_p(lens_a.ctypes.data), ctypes.c_void_p(int(d_out_ptr)),
+                                           out_cap, ctypes.c_void_p(first.ctypes.data),
+                                           ctypes.c_void_p(int(stream))))
+        return first
 
     def batch_max_chunks(self, lens):
         n = len(lens)

@@ -105,7 +105,7 @@ def lib():
     L.cdc_last_error.restype = ctypes.c_char_p
     L.cdc_set_gear.argtypes = [P, u64p]
     L.cdc_set_gear.restype = ctypes.c_int
-    L.cdc_chunk_batch_device.argtypes = [P, sz, ctypes.POINTER(P), u64p, P, sz, u64p, P]
+    L.cdc_chunk_batch_device.argtypes = [P, sz, P, P, P, sz, P, P]
     L.cdc_chunk_batch_device.restype = ctypes.c_int64
     L.cdc_batch_max_chunks.argtypes = [P, sz, u64p]
     L.cdc_batch_max_chunks.restype = sz

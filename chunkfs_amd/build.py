@@ -18,6 +18,20 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 
+def source_digest():
+    """SHA-256 (first 16 hex digits) over every source and header the library
+    is built from: ties a profile under profiles/ to the build it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [
+        os.path.join(ROOT, "include", f) for f in ("chunkfs_amd.h", "chunkfs_amd_tables.h", "chunkfs_amd_debug.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def _newer(target, deps):
     if not os.path.exists(target):
         return True

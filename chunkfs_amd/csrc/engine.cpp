@@ -316,11 +316,18 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
     const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : 0;
     uint64_t spans = 0;
+    multi_span_ = false;
     for (size_t i = 0; i < n; ++i) {
         h_ptrs[i] = reinterpret_cast<uint64_t>(d_streams[i]);
         h_lens[i] = lens[i];
         h_sb[i] = spans;
-        if (algo_ == CDC_ALGO_FASTCDC) spans += (lens[i] + (1ull << sl2) - 1) >> sl2;
+        if (algo_ == CDC_ALGO_FASTCDC) {
+            const uint64_t k = (lens[i] + (1ull << sl2) - 1) >> sl2;
+            spans += k;
+            // Zero-length streams own no span, so spans > n does not imply a
+            // multi-span stream: record it per stream.
+            if (k >= 2) multi_span_ = true;
+        }
     }
     h_sb[n] = spans;
     if (algo_ == CDC_ALGO_FASTCDC && spans == 0) {  // every stream is empty
@@ -366,7 +373,7 @@ int Engine::run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     HIP_TRY(v1::launch_trunc(st, fp_, d_gear_, cand_, s));
     HIP_TRY(v1::launch_spec(st, fp_, d_gear_, cand_, chains1_, comp1_.stats, s));
     int exit_buf = 0;
-    if (st.total_spans > st.n) {  // some stream has >= 2 spans: chains must be joined
+    if (multi_span_) {  // some stream has >= 2 spans: chains must be joined
         // kJacobi device passes (each a no-op once converged) and a serial
         // catch-up that runs only if the last pass still changed an exit: no
         // host round trip on any path.

@@ -121,6 +121,7 @@ class Engine {
     uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
     uint64_t last_spans_ = 0;  // spans of the last FastCDC batch (debug_copy)
     uint64_t out_cap_ = 0;     // capacity of the current batch's output (walk_kernel bound)
+    bool multi_span_ = false;  // some stream of the current batch has >= 2 spans
 };
 
 void set_error(const std::string &msg);

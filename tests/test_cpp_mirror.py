@@ -28,7 +28,6 @@ def test_cpp_mirror_compiles_and_links():
 
 
 @pytest.mark.gpu
-@pytest.mark.xfail(strict=False, reason="first GPU run of the C++ example pending")
 def test_cpp_mirror_runs_on_gpu():
     _build_example()
     r = subprocess.run([EXE], capture_output=True, text=True, timeout=300)

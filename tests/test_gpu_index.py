@@ -16,10 +16,7 @@ import pytest
 
 import oracle
 
-# Added while the GPU pool was unreachable: expected to pass, but reported as
-# xfail/xpass (never stopping an unattended `-m gpu -x` run) until its first GPU run.
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.xfail(strict=False, reason="first GPU run of this kernel pending")]
+pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 

@@ -196,6 +196,19 @@ def test_mixed_entropy_batch():
         assert_same(out[first[i]:first[i + 1]], oracle.fastcdc(a, *sizes), f"stream {i}")
 
 
+@pytest.mark.parametrize("lens", [[0, 100000], [0, 0, 3 * 65536 + 999], [0, 65536 + 1, 0, 200000]])
+def test_empty_streams_next_to_multispan_low_entropy(lens):
+    """Zero-length streams own no span, so they must not hide a multi-span
+    stream from the cross-span join (a span count > stream count test would):
+    all-zero data at (4096, 8192, 20000) makes every guessed chain wrong."""
+    sizes = (4096, 8192, 20000)
+    ch = chunker(sizes)
+    arrays = [np.zeros(n, dtype=np.uint8) for n in lens]
+    out, first = _torch_batch(ch, arrays)
+    for i, a in enumerate(arrays):
+        assert_same(out[first[i]:first[i + 1]], oracle.fastcdc(a, *sizes), f"stream {i} len={len(a)}")
+
+
 def test_batch_composition_invariance():
     """Determinism: a stream's chunks do not depend on what else is in the batch."""
     sizes = SIZES[0]
@@ -247,3 +260,41 @@ def test_one_gib_stream_and_timing():
     # size-independent properties
     assert int(got[:, 1].sum()) == n
     assert (got[:-1, 1] >= sizes[0]).all() and (got[:, 1] <= sizes[2]).all()
+
+
+def test_config4_batch_1024_streams_of_64mib():
+    """BASELINE config 4 on one GPU: 1024 independent 64 MiB streams (64 GiB in
+    HBM), stream i = splitmix64(seed=1000+i), FastCDC 4/8/16 KiB.  A seeded
+    sample of 16 streams is compared bit-exact with the oracle; on all 1024 the
+    size-independent invariants hold: exact tiling from 0, min <= len <= max
+    except each stream's last chunk, first[] monotone with first[0] == 0."""
+    import ctypes
+    import torch
+    from chunkfs_amd import _lib
+    sizes = SIZES[0]
+    ch = chunker(sizes)
+    n_streams, slen = 1024, 64 << 20
+    buf = torch.empty(n_streams * slen, dtype=torch.uint8, device="cuda")
+    L = _lib.lib()
+    for i in range(n_streams):
+        _lib.check(L.cdc_fill_splitmix64_device(ctypes.c_void_p(buf.data_ptr() + i * slen), slen, 1000 + i, None))
+    ptrs = [buf.data_ptr() + i * slen for i in range(n_streams)]
+    lens = [slen] * n_streams
+    cap = ch.batch_max_chunks(lens)
+    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda")
+    first = ch.chunk_batch_device(ptrs, lens, out.data_ptr(), cap)
+    torch.cuda.synchronize()
+    first = np.asarray(first, dtype=np.int64)
+    assert first[0] == 0 and (np.diff(first) > 0).all()
+    got = out[:int(first[-1])].cpu().numpy().view(np.uint64)
+    off, ln = got[:, 0].astype(np.int64), got[:, 1].astype(np.int64)
+    for i in range(n_streams):
+        o, l_ = off[first[i]:first[i + 1]], ln[first[i]:first[i + 1]]
+        assert o[0] == 0 and (o[1:] == np.cumsum(l_)[:-1]).all() and int(l_.sum()) == slen, i
+        assert (l_[:-1] >= sizes[0]).all() and (l_ <= sizes[2]).all(), i
+    rng = np.random.default_rng(4)
+    for i in sorted(rng.choice(n_streams, size=16, replace=False).tolist()):
+        host = buf[i * slen:(i + 1) * slen].cpu().numpy()
+        assert_same(got[first[i]:first[i + 1]], oracle.fastcdc(host, *sizes), f"config4 stream {i}")
+    del buf, out
+    torch.cuda.empty_cache()

@@ -12,10 +12,7 @@ import pytest
 
 import oracle
 
-# Added while the GPU pool was unreachable: expected to pass, but reported as
-# xfail/xpass (never stopping an unattended `-m gpu -x` run) until its first GPU run.
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.xfail(strict=False, reason="first GPU run of this kernel pending")]
+pytestmark = pytest.mark.gpu
 
 
 def _digests(data, chunks):
@@ -68,3 +65,23 @@ def test_fixed_chunker_hash_dedup_known_answer():
     uniq = {bytes(r) for r in dig}
     assert len(uniq) == 512
     assert bytes(dig[0]) == hashlib.sha256(bytes(block[:8192])).digest()
+
+
+def test_config1_fixed_8k_64mib_sha256():
+    """BASELINE config 1: FSChunker 8 KiB over a 64 MiB splitmix64(seed=0x0C0FFEE1)
+    buffer, every chunk fingerprinted (StorageWriter's Sha256Hasher) and put in a
+    HashMap-style unique set: 8192 chunks, average 8192 B, dedup ratio 1.0
+    (SURVEY.md §8d).  All 8192 digests are checked against hashlib."""
+    import chunkfs_amd as c
+    n = 64 << 20
+    data = oracle.splitmix64_bytes(n, 0x0C0FFEE1)
+    ch = c.FSChunker(8192)
+    chunks, dig = ch.chunk_and_hash(data)
+    assert (chunks == oracle.fixed(n, 8192)).all()
+    assert chunks.shape[0] == 8192
+    assert (dig == _digests(data, chunks)).all()
+    unique = {}
+    for (o, ln), d in zip(chunks, dig):
+        unique.setdefault(bytes(d), int(ln))  # database.rs:74-77: first insert wins
+    assert n / sum(unique.values()) == 1.0
+    assert sum(unique.values()) / len(unique) == 8192.0

@@ -1,27 +1,25 @@
 #!/bin/bash
 # PMC passes on the scan kernel (separate rocprofv3 runs, counters only, as
-# MI355X_MICROARCH.md prescribes).  Usage: tools/pmc.sh TAG
-TAG=${1:-r01}
+# MI355X_MICROARCH.md prescribes).  Usage: tools/pmc.sh TAG [kernel-regex]
+TAG=${1:-r02}
+KRE=${2:-scan_kernel}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 run() {  # name, counters...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "scan_kernel" --output-format csv \
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" --output-format csv \
       -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity --no-host-path \
-      > $OUT/$name.log 2>&1
+      --no-sweep > $OUT/$name.log 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   return $rc
 }
-ok() { [ $1 -eq 0 ] || [ $1 -eq 1 ]; }
-run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY; ok $? || exit 1
-run sq2 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT; ok $? || exit 1
-run sq3 SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_INSTS_VALU_INT64 SQ_INST_LEVEL_LDS SQ_BUSY_CU_CYCLES SQ_THREAD_CYCLES_VALU; ok $? || exit 1
-run ta TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum; ok $? || true
-run fetch FETCH_SIZE; ok $? || exit 1
-run tcc TCC_HIT_sum TCC_MISS_sum; ok $? || exit 1
+run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY || exit 1
+run sq2 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
+run sq3 SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_INT64 SQ_INST_LEVEL_LDS SQ_BUSY_CU_CYCLES || exit 1
+run fetch FETCH_SIZE || exit 1
+run tcc TCC_HIT_sum TCC_MISS_sum || exit 1
 for d in $OUT/*/; do f=$(find $d -name "*counter_collection.csv" | head -1); [ -n "$f" ] && echo "== $d" && python3 - "$f" <<'PY'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))

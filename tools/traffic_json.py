@@ -7,10 +7,17 @@ bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, "HBM [CDNA4]"):
 bytes = FETCH_SIZE * 1024 * 2.
 
 usage: tools/traffic_json.py <fetch counter_collection.csv> <out.json> [workload_bytes]
+
+The JSON records the library's source digest (chunkfs_amd.build.source_digest)
+so bench.py only quotes traffic measured on the build that is running.
 """
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from chunkfs_amd import build  # noqa: E402
 
 
 def main():
@@ -27,6 +34,7 @@ def main():
     out = {
         "kernel": "scan_kernel",
         "kernel_symbol": name,
+        "source_digest": build.source_digest(),
         "workload_bytes": workload,
         "dispatches": len(vals),
         "fetch_size_kib_mean": sum(vals) / len(vals),

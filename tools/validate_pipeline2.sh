@@ -11,16 +11,16 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 ok() { [ $1 -eq 0 ] || [ $1 -eq 1 ]; }
 
-CHUNKFS_AMD_TEST_PIPELINE2=1 timeout -k 10 600 python -m pytest tests/test_gpu_pipeline2.py -m gpu -q -x \
-    --timeout 120 -k "stage" > $OUT/p2_stage_$TAG.log 2>&1
+CHUNKFS_AMD_TEST_PIPELINE2=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline2.py -m gpu -v -x \
+    --timeout 120 --timeout-method thread -k "stage" > $OUT/p2_stage_$TAG.log 2>&1
 rc=$?; echo "stage rc=$rc"; tail -20 $OUT/p2_stage_$TAG.log; ok $rc || exit $rc
 
-CHUNKFS_AMD_TEST_PIPELINE2=1 timeout -k 10 900 python -m pytest tests/test_gpu_pipeline2.py -m gpu -q \
-    --timeout 300 > $OUT/p2_parity_$TAG.log 2>&1
+CHUNKFS_AMD_TEST_PIPELINE2=1 timeout -k 10 900 python -u -m pytest tests/test_gpu_pipeline2.py -m gpu -v \
+    --timeout 300 --timeout-method thread > $OUT/p2_parity_$TAG.log 2>&1
 rc=$?; echo "p2 parity rc=$rc"; tail -20 $OUT/p2_parity_$TAG.log; ok $rc || exit $rc
 
-timeout -k 10 600 python -m pytest tests/test_gpu_sha256.py tests/test_gpu_index.py tests/test_cpp_mirror.py \
-    -m gpu -q -rxX --timeout 300 > $OUT/new_kernels_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sha256.py tests/test_gpu_index.py tests/test_cpp_mirror.py \
+    -m gpu -v -rxX --timeout 300 --timeout-method thread > $OUT/new_kernels_$TAG.log 2>&1
 rc=$?; echo "sha/index/cpp rc=$rc"; tail -20 $OUT/new_kernels_$TAG.log; ok $rc || exit $rc
 
 CHUNKFS_AMD_PIPELINE=2 timeout -k 10 400 python bench.py --steps 20 --warmup 3 --hash > $OUT/bench_p2_$TAG.json 2> $OUT/bench_p2_$TAG.err
