@@ -14,6 +14,7 @@
 #include <cstring>
 
 #include "../../include/chunkfs_amd_tables.h"
+#include "fastcdc.hpp"
 #include "sha256.hpp"
 
 namespace cdc {
@@ -67,7 +68,10 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
     e->avg_ = avg;
     e->max_ = max;
     e->device_ = device;
-    if (const char *pv = std::getenv("CHUNKFS_AMD_PIPELINE")) e->pipeline_ = std::atoi(pv) == 2 ? 2 : 1;
+    if (const char *pv = std::getenv("CHUNKFS_AMD_PIPELINE")) {
+        const int v = std::atoi(pv);
+        e->pipeline_ = (v == 1 || v == 2) ? v : 3;
+    }
     if (algo == CDC_ALGO_FASTCDC) {
         if (min < kMinimumMin || min > kMinimumMax || avg < kAverageMin ||
             avg > kAverageMax || max < kMaximumMin || max > kMaximumMax) {
@@ -199,8 +203,8 @@ int Engine::ensure_host_staging(size_t n) {
     (void)hipHostFree(h_stage_);
     h_stage_ = nullptr;
     const size_t want = n + 64;
-    // ptrs[n] lens[n] span_base[n+1] | stats[4] first[n+1] (fixed: first[n+1])
-    HIP_TRY(hipHostMalloc(&h_stage_, (4 * want + 16) * sizeof(uint64_t), hipHostMallocCoherent));
+    // ptrs[W] lens[W] span_base[W] tails[W] | stats ++ first[n+1] (fixed: first[n+1])
+    HIP_TRY(hipHostMalloc(&h_stage_, (5 * want + 32) * sizeof(uint64_t), hipHostMallocCoherent));
     h_stage_streams_ = want;
     return CDC_OK;
 }
@@ -228,6 +232,11 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     const size_t o1_changed = take(16), o1_ci = take((S + 1) * 8), o1_bs = take((S / 1024 + 2) * 8);
     const size_t o1_stats = take((4 + N + 1) * 8);  // stats[4] ++ first[N+1]: one D2H
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
+    // pipeline 3 (fastcdc.hip) state; its chunk starts share o_st0
+    const size_t o3_nst = take(S * 4), o3_ent = take(S * 8), o3_ex = take(S * 8);
+    const size_t o3_bx0 = take((S / 64 + 2) * 8), o3_bx1 = take((S / 64 + 2) * 8);
+    const size_t o3_bsum = take((S / 1024 + 2) * 8), o3_stats = take(p3::kStatWords * 8);
+    const size_t o3_tails = take(N * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
     ws_spans_ = 0;
@@ -267,6 +276,16 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
+    ch3_.smax = (uint32_t)smax;
+    ch3_.starts = chains_.starts[0];
+    ch3_.nst = reinterpret_cast<uint32_t *>(b + o3_nst);
+    ch3_.ent = reinterpret_cast<uint64_t *>(b + o3_ent);
+    ch3_.ex = reinterpret_cast<uint64_t *>(b + o3_ex);
+    ch3_.bx[0] = reinterpret_cast<uint64_t *>(b + o3_bx0);
+    ch3_.bx[1] = reinterpret_cast<uint64_t *>(b + o3_bx1);
+    cp3_.bsum = reinterpret_cast<uint64_t *>(b + o3_bsum);
+    cp3_.stats = reinterpret_cast<uint64_t *>(b + o3_stats);
+    d_tails_ = reinterpret_cast<uint64_t *>(b + o3_tails);
     return CDC_OK;
 }
 
@@ -314,8 +333,10 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     if (rc) return rc;
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
+    uint64_t *h_tails = h + 3 * h_stage_streams_;
     const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : 0;
     uint64_t spans = 0;
+    uint32_t n_tails = 0;
     multi_span_ = false;
     for (size_t i = 0; i < n; ++i) {
         h_ptrs[i] = reinterpret_cast<uint64_t>(d_streams[i]);
@@ -324,6 +345,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
         if (algo_ == CDC_ALGO_FASTCDC) {
             const uint64_t k = (lens[i] + (1ull << sl2) - 1) >> sl2;
             spans += k;
+            if (lens[i] & ((1ull << sl2) - 1)) h_tails[n_tails++] = spans - 1;  // ragged last span
             // Zero-length streams own no span, so spans > n does not imply a
             // multi-span stream: record it per stream.
             if (k >= 2) multi_span_ = true;
@@ -345,6 +367,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
         HIP_TRY(hipMemcpyAsync(d_ptrs_, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_lens_, h_lens, n * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_span_base_, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
+        if (n_tails) HIP_TRY(hipMemcpyAsync(d_tails_, h_tails, n_tails * 8, hipMemcpyHostToDevice, s));
         tables_.assign(h_ptrs, h_ptrs + n);
         tables_.insert(tables_.end(), h_lens, h_lens + n);
         tables_gen_ = ws_gen_;
@@ -357,6 +380,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     st.span_log2 = sl2;
     st.total_spans = spans;
     last_spans_ = algo_ == CDC_ALGO_FASTCDC ? spans : 0;
+    n_tails_ = n_tails;
     rc = algo_ == CDC_ALGO_FASTCDC ? run_fast(st, d_out, n, first, s)
                                    : run_fixed(st, n, lens, d_out, first, s);
     if (rc) return rc;
@@ -366,7 +390,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
 int Engine::run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                         uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1]
+    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats[4] ++ first[n+1]
     HIP_TRY(hipEventRecord(ev_[0], s));
     HIP_TRY(v1::launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
@@ -409,11 +433,55 @@ int Engine::run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     return CDC_OK;
 }
 
+int Engine::run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+                        uint64_t *first, hipStream_t s) {
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats ++ first[n+1], written by the device
+    p3::Compact cp = cp3_;
+    cp.h_stats = h_misc;
+    cp.h_first = h_misc + p3::kStatWords;
+    h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the last write_kernel block
+    HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, d_tails_, n_tails_, num_cus_, s));
+    HIP_TRY(hipEventRecord(ev_[1], s));
+    HIP_TRY(p3::launch_chain(st, fp_, d_gear_, cand_, ch3_, cp, s));
+    HIP_TRY(p3::launch_fix(st, fp_, d_gear_, cand_, ch3_, cp, s));
+    HIP_TRY(hipEventRecord(ev_[2], s));
+    HIP_TRY(p3::launch_compact(st, ch3_, cp, d_out, out_cap_, s));
+    HIP_TRY(hipEventRecord(ev_[3], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
+        set_error(h_misc[p3::kStatDone] != 1 ? "compaction kernel did not report back"
+                                             : "chain overflow or output bound hit (internal error)");
+        return CDC_EDEVICE;
+    }
+    // Zero-length streams own no span: their first[] is the next stream's.
+    const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
+    uint64_t *hf = h_misc + p3::kStatWords;
+    for (size_t i = n; i-- > 0;)
+        if (lens[i] == 0) hf[i] = hf[i + 1];
+    std::memcpy(first, hf, (n + 1) * 8);
+    float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
+    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
+    HIP_TRY(hipEventElapsedTime(&t23, ev_[2], ev_[3]));
+    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
+    timing_.scan_ms = t01;
+    timing_.resolve_ms = t12;
+    timing_.compact_ms = t23;
+    timing_.total_ms = t03;
+    timing_.candidates = h_misc[p3::kStatCand];
+    timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
+    timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk] + (h_misc[p3::kStatSerial] ? 1000000u : 0u);
+    return CDC_OK;
+}
+
 int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                      uint64_t *first, hipStream_t s) {
+    if (pipeline_ == 3) return run_fast_v3(st, d_out, n, first, s);
     if (pipeline_ == 1) return run_fast_v1(st, d_out, n, first, s);
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_misc = h + 3 * h_stage_streams_;  // stats[4] ++ first[n+1], written by the device
+    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats[4] ++ first[n+1], written by the device
     Lookback lb = lb_;
     lb.h_stats = h_misc;
     lb.h_first = h_misc + 4;
@@ -453,7 +521,7 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
 int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                       cdc_chunk_t *d_out, uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_first = h + 3 * h_stage_streams_;
+    uint64_t *h_first = h + 4 * h_stage_streams_;
     uint64_t t = 0;
     for (size_t i = 0; i < n; ++i) {
         h_first[i] = t;

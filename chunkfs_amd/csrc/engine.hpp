@@ -12,6 +12,7 @@
 
 #include "../../include/chunkfs_amd.h"
 #include "cdc_kernels.hpp"
+#include "fastcdc.hpp"
 #include "pipeline_v1.hpp"
 
 namespace cdc {
@@ -62,6 +63,8 @@ class Engine {
                  uint64_t *first, hipStream_t s);
     int run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                     uint64_t *first, hipStream_t s);
+    int run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+                    uint64_t *first, hipStream_t s);
     int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                   cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
 
@@ -73,7 +76,7 @@ class Engine {
     // FastCDC pipeline: 1 = pipeline_v1.hip (GPU-validated, default), 2 =
     // cdc_kernels.hip (per-lane sub-span scan, record links + lane walk);
     // environment CHUNKFS_AMD_PIPELINE at cdc_create.
-    int pipeline_ = 1;
+    int pipeline_ = 3;
     uint32_t span_log2_ = 16;
     uint32_t cap_ = 0, smax_ = 0;
     std::string describe_;
@@ -92,6 +95,10 @@ class Engine {
     Lookback lb_{};
     v1::Chains chains1_{};         // pipeline 1 (pipeline_v1.hip)
     v1::Compact comp1_{};
+    p3::Chains ch3_{};             // pipeline 3 (fastcdc.hip, default)
+    p3::Compact cp3_{};
+    uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids
+    uint32_t n_tails_ = 0;
     uint64_t *d_nxt_ = nullptr;    // [spans*cap] record links (next_kernel)
     uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
     const uint8_t **d_ptrs_ = nullptr;
