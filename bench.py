@@ -151,7 +151,7 @@ class StubEngine:
         return first
 
     def timing(self):
-        return {"scan_ms": 0.0, "total_ms": 0.0, "resolve_ms": 0.0, "fixup_iterations": 0}
+        return {"scan_ms": 0.0, "total_ms": 0.0, "resolve_ms": 0.0, "fixup_iterations": 0, "walk_fallback_steps": 0}
 
     def sync(self):
         pass
@@ -345,7 +345,7 @@ def main(argv=None):
     if world > 1:
         dist.barrier()
     eng.sync()
-    scan_ms, total_ms, resolve_ms, rewalked = [], [], [], []
+    scan_ms, total_ms, resolve_ms, rewalked, fallback = [], [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         first = eng.step()
@@ -354,6 +354,7 @@ def main(argv=None):
         total_ms.append(t["total_ms"])
         resolve_ms.append(t["resolve_ms"])
         rewalked.append(t["fixup_iterations"])
+        fallback.append(t.get("walk_fallback_steps", 0))
     eng.sync()
     if world > 1:
         dist.barrier()
@@ -432,7 +433,8 @@ def main(argv=None):
             },
             "cpu_baseline": extras.pop("cpu_baseline", None),
             "phase_ms": {"scan": scan_avg_ms, "total_device": sum(total_ms) / len(total_ms),
-                         "resolve": sum(resolve_ms) / len(resolve_ms), "rewalked_spans": max(rewalked)},
+                         "resolve": sum(resolve_ms) / len(resolve_ms), "rewalked_spans": max(rewalked),
+                         "walk_fallback_steps": max(fallback)},
         }
         line.update(extras)
         if args.stub:

@@ -57,6 +57,7 @@ class cdc_timing_t(ctypes.Structure):
         ("candidates", ctypes.c_uint64),
         ("bytes", ctypes.c_uint64),
         ("hash_ms", ctypes.c_double),
+        ("walk_fallback_steps", ctypes.c_uint64),
     ]
 
 

@@ -49,6 +49,7 @@ struct FastParams {
     uint32_t cm32;           // aligned: (cmask << tshift) >> 32
     uint32_t cm_lo, cm_hi;   // general form
     uint64_t mask_s_sh, mask_l_sh;  // mask_s / mask_l << tshift (exact flush tests)
+    uint32_t diag;           // timing experiments only (CHUNKFS_AMD_DIAG); 0 in every real run
 };
 
 struct Candidates {

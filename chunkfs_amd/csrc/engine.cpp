@@ -104,6 +104,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         fp.cm_hi = (uint32_t)(fp.cmask >> 32);
         fp.mask_s_sh = fp.mask_s << fp.tshift;
         fp.mask_l_sh = fp.mask_l << fp.tshift;
+        if (const char *d = std::getenv("CHUNKFS_AMD_DIAG")) fp.diag = (uint32_t)std::atoi(d);
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
         const uint64_t span = 1ull << e->span_log2_;
@@ -233,9 +234,8 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     const size_t o1_stats = take((4 + N + 1) * 8);  // stats[4] ++ first[N+1]: one D2H
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     // pipeline 3 (fastcdc.hip) state; its chunk starts share o_st0
-    const size_t o3_nst = take(S * 4), o3_ent = take(S * 8), o3_ex = take(S * 8);
-    const size_t o3_bx0 = take((S / 64 + 2) * 8), o3_bx1 = take((S / 64 + 2) * 8);
-    const size_t o3_bsum = take((S / 1024 + 2) * 8), o3_stats = take(p3::kStatWords * 8);
+    const uint64_t nb3 = p3::resolve_blocks(S) + 2;
+    const size_t o3_stats = take(p3::kStatWords * 8), o3_desc = take(6 * nb3 * 8);
     const size_t o3_tails = take(N * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
@@ -278,13 +278,11 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
     ch3_.smax = (uint32_t)smax;
     ch3_.starts = chains_.starts[0];
-    ch3_.nst = reinterpret_cast<uint32_t *>(b + o3_nst);
-    ch3_.ent = reinterpret_cast<uint64_t *>(b + o3_ent);
-    ch3_.ex = reinterpret_cast<uint64_t *>(b + o3_ex);
-    ch3_.bx[0] = reinterpret_cast<uint64_t *>(b + o3_bx0);
-    ch3_.bx[1] = reinterpret_cast<uint64_t *>(b + o3_bx1);
-    cp3_.bsum = reinterpret_cast<uint64_t *>(b + o3_bsum);
     cp3_.stats = reinterpret_cast<uint64_t *>(b + o3_stats);
+    uint64_t *desc = reinterpret_cast<uint64_t *>(b + o3_desc);
+    rs3_ = p3::Resolve{desc,           desc + nb3,     desc + 2 * nb3, desc + 3 * nb3,
+                       desc + 4 * nb3, desc + 5 * nb3, 0};
+    HIP_TRY(hipMemset(desc, 0, 6 * nb3 * 8));  // no stale status word can carry a live generation
     d_tails_ = reinterpret_cast<uint64_t *>(b + o3_tails);
     return CDC_OK;
 }
@@ -440,20 +438,26 @@ int Engine::run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     p3::Compact cp = cp3_;
     cp.h_stats = h_misc;
     cp.h_first = h_misc + p3::kStatWords;
-    h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the last write_kernel block
+    h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the last resolve block
+    p3::Resolve rs = rs3_;
+    rs.gen = ++res_gen_;
     HIP_TRY(hipEventRecord(ev_[0], s));
     HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, d_tails_, n_tails_, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
-    HIP_TRY(p3::launch_chain(st, fp_, d_gear_, cand_, ch3_, cp, s));
-    HIP_TRY(p3::launch_fix(st, fp_, d_gear_, cand_, ch3_, cp, s));
+    HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, ch3_, cp, rs, d_out, out_cap_, s));
     HIP_TRY(hipEventRecord(ev_[2], s));
-    HIP_TRY(p3::launch_compact(st, ch3_, cp, d_out, out_cap_, s));
-    HIP_TRY(hipEventRecord(ev_[3], s));
     HIP_TRY(hipStreamSynchronize(s));
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
-        set_error(h_misc[p3::kStatDone] != 1 ? "compaction kernel did not report back"
-                                             : "chain overflow or output bound hit (internal error)");
+        set_error(h_misc[p3::kStatDone] != 1 ? "resolve kernel did not report back"
+                                             : "chain overflow, output bound or look-back timeout (internal error)");
         return CDC_EDEVICE;
+    }
+    if (fp_.diag & 128) {
+        const double waves = (double)p3::resolve_blocks(st.total_spans) * 4;
+        std::fprintf(stderr, "resolve phases, us per wave (meta recs trunc links virt walk lookback out):");
+        for (int i = 0; i < p3::kStatDiagN; ++i)
+            std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / waves);
+        std::fprintf(stderr, "\n");
     }
     // Zero-length streams own no span: their first[] is the next stream's.
     const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
@@ -461,18 +465,18 @@ int Engine::run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     for (size_t i = n; i-- > 0;)
         if (lens[i] == 0) hf[i] = hf[i + 1];
     std::memcpy(first, hf, (n + 1) * 8);
-    float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
+    float t01 = 0, t12 = 0, t02 = 0;
     HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
     HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
-    HIP_TRY(hipEventElapsedTime(&t23, ev_[2], ev_[3]));
-    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
+    HIP_TRY(hipEventElapsedTime(&t02, ev_[0], ev_[2]));
     timing_.scan_ms = t01;
     timing_.resolve_ms = t12;
-    timing_.compact_ms = t23;
-    timing_.total_ms = t03;
+    timing_.compact_ms = 0;  // fused into the resolve kernel
+    timing_.total_ms = t02;
     timing_.candidates = h_misc[p3::kStatCand];
     timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
-    timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk] + (h_misc[p3::kStatSerial] ? 1000000u : 0u);
+    timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk];
+    timing_.walk_fallback_steps = h_misc[p3::kStatOnDemand];
     return CDC_OK;
 }
 

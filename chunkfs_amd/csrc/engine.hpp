@@ -97,6 +97,8 @@ class Engine {
     v1::Compact comp1_{};
     p3::Chains ch3_{};             // pipeline 3 (fastcdc.hip, default)
     p3::Compact cp3_{};
+    p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
+    uint64_t res_gen_ = 0;
     uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids
     uint32_t n_tails_ = 0;
     uint64_t *d_nxt_ = nullptr;    // [spans*cap] record links (next_kernel)

@@ -6,29 +6,28 @@
 // depends on the previous one through the min-skip and the hash reset; the GPU
 // splits the work into a data-parallel HBM pass and a small resolve:
 //
-//  scan_kernel    for EVERY position i the windowed gear hash W_i (bits
-//                 0..47 exact: the masks never test bit 48 or above) and a
-//                 candidate record where (W_i & (mask_s & mask_l)) == 0.
-//                 Wave per span; lane l owns the contiguous 1 KiB segment
-//                 [l*sub, (l+1)*sub) and hashes it serially (one v_lshl_add_u64
-//                 per byte).  The bytes arrive with fully coalesced loads --
-//                 each wave-instruction reads 16 complete 64-byte pieces --
-//                 and are transposed to their owning lanes through a 4 KiB
-//                 per-wave LDS tile (tools/ubench_scan.hip: lane-strided loads
-//                 cap the read rate at 4.1 TB/s, grouped ones reach 6.0).
-//                 A lane starts from hash 0 and re-tests its first 48
-//                 positions at the end, with the true carry-in taken from
-//                 lane l-1 by one DPP shift: no warm-up bytes are re-read.
-//  chain_kernel   wave per span: the exact successor ("link") of every
-//                 candidate record in reach, lane per record, then a chain
-//                 walk over those links from a warm-up start before the span.
-//  fix_kernel     Jacobi passes over 64-span blocks: spans whose speculative
-//                 entry differs from their predecessor's exit are re-walked.
-//  serial_kernel  the same, one wave over all blocks in order, only when the
-//                 passes did not converge (degenerate data).
-//  count/write    chunk-count prefix and the Chunk{offset,length} output.
+//  scan_kernel     for EVERY position i the windowed gear hash W_i (bits
+//                  0..47 exact: the masks never test bit 48 or above) and a
+//                  candidate record where (W_i & (mask_s & mask_l)) == 0.
+//                  Wave per span; lane l owns the contiguous 1 KiB segment
+//                  [l*sub, (l+1)*sub) and hashes it serially (one v_lshl_add_u64
+//                  per byte).  The bytes arrive with fully coalesced loads --
+//                  each wave-instruction reads 16 complete 64-byte pieces --
+//                  and are transposed to their owning lanes through a 4 KiB
+//                  per-wave LDS tile (tools/ubench_scan.hip: lane-strided loads
+//                  cap the read rate at 4.1 TB/s, grouped ones reach 6.0).
+//                  A lane starts from hash 0 and re-tests its first 48
+//                  positions at the end, with the true carry-in taken from
+//                  lane l-1 by one DPP shift: no warm-up bytes are re-read.
+//  resolve_kernel  everything after the scan in one launch, block per 32
+//                  spans: the exact successor ("link") of every candidate
+//                  record in reach, chain walks over those links from a
+//                  warm-up start before each span, a decoupled look-back over
+//                  blocks for the chunk-count prefix and the block-boundary
+//                  check, and the Chunk{offset,length} output.
 #include "fastcdc.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace cdc {
@@ -47,6 +46,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
 typedef const __attribute__((address_space(1))) uint8_t g_u8;
 typedef const __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint64_t g_u64;
 __device__ __forceinline__ g_u32x4 *as_global4(const void *p) { return (g_u32x4 *)(p); }
 __device__ __forceinline__ g_u8 *as_global1(const void *p) { return (g_u8 *)(p); }
 __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
@@ -116,10 +116,29 @@ __device__ __forceinline__ uint64_t gear_prefix(uint64_t g, uint32_t lane) {
     return g;
 }
 
+constexpr uint32_t kTruncMax = 47;    // mask bits <= 47 (checked on the host)
+constexpr uint32_t kTruncNone = 63;   // truncated-region result: no hit
+
+struct Regime {
+    uint64_t rem, a0, ce, re, tl;
+};
+
+// Chunk regime at start s (SURVEY.md A.2): rem clipped to max, centre, and
+// the even-rounded scan bounds; tl = end of the truncated positions.
+__device__ __forceinline__ Regime regime(const FastParams &fp, uint64_t s, uint64_t n) {
+    Regime R;
+    uint64_t rem = n - s, center = fp.avg;
+    if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
+    R.rem = rem;
+    R.a0 = (fp.min / 2) * 2;
+    R.ce = (center / 2) * 2;
+    R.re = (rem / 2) * 2;
+    R.tl = min(R.a0 + (uint64_t)fp.trunc, R.re);
+    return R;
+}
+
 // ---- scan ------------------------------------------------------------------
 
-constexpr int kScanThreads = 1024;    // 16 waves, one block per CU (LDS-bound)
-constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kCopies = 32;           // GEAR replicas: lane&31 picks a bank pair
 constexpr uint32_t kEntCap = 64;      // per-wave list of hitting 16-byte quarters per span
 constexpr uint32_t kStep = 64;        // bytes per lane per step (4 quarters)
@@ -223,31 +242,59 @@ struct Q4 {
     uint4 q[4];
 };
 
-template <bool kAlign>
+template <bool kAlign, int kLook>
 __device__ __forceinline__ void process_step(const Q4 &C, uint64_t &h, uint32_t pos0, uint32_t skip, uint32_t &ne,
                                              const EntryList &E, const uint64_t *tab, uint32_t rep,
                                              const FastParams &fp) {
-    G4 ga, gb;
-    look4(ga, tab, rep, C.q[0].x);
-    SCHED_FENCE();
+    if constexpr (kLook == 1) {
+        G4 ga, gb;
+        look4(ga, tab, rep, C.q[0].x);
+        SCHED_FENCE();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint64_t h0 = h;
-        uint32_t acc = 0xffffffffu;
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t h0 = h;
+            uint32_t acc = 0xffffffffu;
 #pragma unroll
-        for (int w = 0; w < 4; w += 2) {
-            look4(gb, tab, rep, word_of(C.q[q], w + 1));
-            SCHED_FENCE();
-            chain4_test<kAlign>(h, acc, ga, fp);
-            SCHED_FENCE();
-            if (q < 3 || w < 2) {
-                look4(ga, tab, rep, w < 2 ? word_of(C.q[q], w + 2) : word_of(C.q[q + 1], 0));
+            for (int w = 0; w < 4; w += 2) {
+                look4(gb, tab, rep, word_of(C.q[q], w + 1));
+                SCHED_FENCE();
+                chain4_test<kAlign>(h, acc, ga, fp);
+                SCHED_FENCE();
+                if (q < 3 || w < 2) {
+                    look4(ga, tab, rep, w < 2 ? word_of(C.q[q], w + 2) : word_of(C.q[q + 1], 0));
+                    SCHED_FENCE();
+                }
+                chain4_test<kAlign>(h, acc, gb, fp);
                 SCHED_FENCE();
             }
-            chain4_test<kAlign>(h, acc, gb, fp);
-            SCHED_FENCE();
+            append_hits(acc == 0 && (uint32_t)q >= skip, pos0 + 16 * q, h0, ne, E);
         }
-        append_hits(acc == 0 && (uint32_t)q >= skip, pos0 + 16 * q, h0, ne, E);
+    } else {
+        // two dwords (8 lookups) ahead of the chain
+        G4 ga0, ga1, gb0, gb1;
+        look4(ga0, tab, rep, C.q[0].x);
+        look4(ga1, tab, rep, C.q[0].y);
+        SCHED_FENCE();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t h0 = h;
+            uint32_t acc = 0xffffffffu;
+            look4(gb0, tab, rep, C.q[q].z);
+            look4(gb1, tab, rep, C.q[q].w);
+            SCHED_FENCE();
+            chain4_test<kAlign>(h, acc, ga0, fp);
+            chain4_test<kAlign>(h, acc, ga1, fp);
+            SCHED_FENCE();
+            if (q < 3) {
+                look4(ga0, tab, rep, C.q[q + 1].x);
+                look4(ga1, tab, rep, C.q[q + 1].y);
+                SCHED_FENCE();
+            }
+            chain4_test<kAlign>(h, acc, gb0, fp);
+            chain4_test<kAlign>(h, acc, gb1, fp);
+            SCHED_FENCE();
+            append_hits(acc == 0 && (uint32_t)q >= skip, pos0 + 16 * q, h0, ne, E);
+        }
     }
 }
 
@@ -326,28 +373,29 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
     wave_sync_lds();
 }
 
+template <int kW>
 struct ScanLds {
-    uint64_t tab[256 * kCopies];           // 64 KiB: entry e, replica c at e*32+c (LDS address 0)
-    uint4 stage[kScanWaves][64 * 5];       // 80 KiB: per-wave transpose tile, 80-byte rows
-    uint32_t epos[kScanWaves][kEntCap];    // 16 KiB: hitting quarters of the current span
-    uint32_t ehlo[kScanWaves][kEntCap];
-    uint32_t ehhi[kScanWaves][kEntCap];
-    uint32_t ecnt[kScanWaves][kEntCap];
+    uint64_t tab[256 * kCopies];     // 64 KiB: entry e, replica c at e*32+c (LDS address 0)
+    uint4 stage[kW][64 * 5];         // 5 KiB per wave: transpose tile, 80-byte rows
+    uint32_t epos[kW][kEntCap];      // 1 KiB per wave: hitting quarters of the current span
+    uint32_t ehlo[kW][kEntCap];
+    uint32_t ehhi[kW][kEntCap];
+    uint32_t ecnt[kW][kEntCap];
 };
 
 // Full spans.  Lane l owns the contiguous segment [l*sub, (l+1)*sub) and
 // hashes it serially from hash 0; its first 48 positions are re-tested at the
 // end with the true carry-in (lane l-1's final hash, one DPP shift; lane 0's
 // from the 48 bytes before the span).  Ragged last spans: scan_tail_kernel.
-template <bool kAlign>
-__global__ __launch_bounds__(kScanThreads, 1) void scan_kernel(const StreamTable st, const FastParams fp,
-                                                                const uint64_t *__restrict__ gear,
-                                                                const Candidates cand, const Compact cp) {
-    __shared__ ScanLds L;
+template <bool kAlign, int kW, int kLook>
+__global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, const FastParams fp,
+                                                           const uint64_t *__restrict__ gear,
+                                                           const Candidates cand, const Compact cp) {
+    __shared__ ScanLds<kW> L;
     const uint64_t *tab = L.tab;
-    for (int i = threadIdx.x; i < 256 * kCopies; i += kScanThreads)
+    for (int i = threadIdx.x; i < 256 * kCopies; i += kW * 64)
         L.tab[i] = gear[i / kCopies] << fp.tshift;  // pre-shifted GEAR (see FastParams)
-    if (blockIdx.x == 0 && threadIdx.x < kStatWords) cp.stats[threadIdx.x] = 0;  // later kernels accumulate
+    if (blockIdx.x == 0 && threadIdx.x < kStatWords) cp.stats[threadIdx.x] = 0;  // the resolve accumulates
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63;
@@ -363,58 +411,75 @@ __global__ __launch_bounds__(kScanThreads, 1) void scan_kernel(const StreamTable
     uint4 *wrow = &L.stage[wave][(lane >> 2) * 5 + (lane & 3)];
     const uint4 *rrow = &L.stage[wave][lane * 5];
 
-    for (uint64_t g = (uint64_t)blockIdx.x * kScanWaves + wave; g < st.total_spans;
-         g += (uint64_t)gridDim.x * kScanWaves) {
-        uint32_t si;
-        uint64_t off;
-        locate(st, g, si, off);
-        const uint8_t *base = st.ptrs[si] + off;
-        if (st.lens[si] - off < span) continue;  // ragged last span: scan_tail_kernel
+    // Spans are software-pipelined: the first two steps of the next span are
+    // in flight while this span's fix-up and flush run.  Ragged last spans:
+    // scan_tail_kernel.
+    const uint64_t gstride = (uint64_t)gridDim.x * kW;
+    auto next_full = [&](uint64_t g, uint32_t &si, uint64_t &off) {
+        for (; g < st.total_spans; g += gstride) {
+            locate(st, g, si, off);
+            if (st.lens[si] - off >= span) break;
+        }
+        return g;
+    };
+    Q4 A, B, C;
+    uint32_t si, wb = 0;
+    uint64_t off;
+    uint64_t g = next_full((uint64_t)blockIdx.x * kW + wave, si, off);
+    const uint8_t *base = nullptr, *gp = nullptr;
+    auto prefetch = [&]() {  // first two steps and the carry bytes of span g
+        base = st.ptrs[si] + off;
+        gp = base + (uint64_t)(lane >> 2) * sub + (lane & 3) * 16;
+        wb = 0;
+        if (off != 0 && lane < 48) wb = as_global1(base)[(int)lane - 48];
+        gload_step(A, gp, istride, 0);
+        SCHED_FENCE();
+        gload_step(B, gp, istride, 1);
+        SCHED_FENCE();
+    };
+    if (g < st.total_spans) prefetch();
+    while (g < st.total_spans) {
         uint32_t ne = 0;  // quarter entries appended this span (wave-uniform)
         uint64_t h = 0;
-        // Lane 0's carry-in: the true hash of the 48 bytes before the span
-        // (zero at a stream start), one byte per lane + a shuffle scan.
-        uint32_t wb = 0;
-        if (off != 0 && lane < 48) wb = as_global1(base)[(int)lane - 48];
-        const uint8_t *gp = base + (uint64_t)(lane >> 2) * sub + (lane & 3) * 16;
-        Q4 A, B, C;
         uint4 F0, F1, F2;
         // Two steps in flight while one is hashed (A/B ring).  The loop body
         // issues its loads unconditionally -- a conditional load leaves the
         // compiler unsure how many are outstanding at the back edge, and it
         // then waits for all of them -- so the last two steps are peeled.
-        gload_step(A, gp, istride, 0);
-        SCHED_FENCE();
-        gload_step(B, gp, istride, 1);
-        SCHED_FENCE();
         stage_step(C, A, wrow, rrow);
         F0 = C.q[0];
         F1 = C.q[1];
         F2 = C.q[2];
         gload_step(A, gp, istride, 2);
         SCHED_FENCE();
-#define CDC_SCAN_PAIR(T, LOAD_B, STAGE_A, LOAD_A)                                   \
-    do {                                                                            \
-        process_step<kAlign>(C, h, lo + (T) * kStep, (T) == 0 ? 3u : 0u, ne, E, tab, rep, fp); \
-        SCHED_FENCE();                                                              \
-        stage_step(C, B, wrow, rrow);                                               \
-        if (LOAD_B) gload_step(B, gp, istride, (T) + 3);                            \
-        SCHED_FENCE();                                                              \
-        process_step<kAlign>(C, h, lo + ((T) + 1) * kStep, 0u, ne, E, tab, rep, fp); \
-        SCHED_FENCE();                                                              \
-        if (STAGE_A) stage_step(C, A, wrow, rrow);                                  \
-        if (LOAD_A) gload_step(A, gp, istride, (T) + 4);                            \
-        SCHED_FENCE();                                                              \
+#define CDC_SCAN_PAIR(T, LOAD_B, STAGE_A, LOAD_A)                                              \
+    do {                                                                                       \
+        process_step<kAlign, kLook>(C, h, lo + (T) * kStep, (T) == 0 ? 3u : 0u, ne, E, tab, rep, fp); \
+        SCHED_FENCE();                                                                         \
+        stage_step(C, B, wrow, rrow);                                                          \
+        if (LOAD_B) gload_step(B, gp, istride, (T) + 3);                                       \
+        SCHED_FENCE();                                                                         \
+        process_step<kAlign, kLook>(C, h, lo + ((T) + 1) * kStep, 0u, ne, E, tab, rep, fp);    \
+        SCHED_FENCE();                                                                         \
+        if (STAGE_A) stage_step(C, A, wrow, rrow);                                             \
+        if (LOAD_A) gload_step(A, gp, istride, (T) + 4);                                       \
+        SCHED_FENCE();                                                                         \
     } while (0)
         uint32_t t = 0;
         for (; t + 4 < steps; t += 2) CDC_SCAN_PAIR(t, true, true, true);
         CDC_SCAN_PAIR(t, true, true, false);        // steps-4, steps-3
         CDC_SCAN_PAIR(t + 2, false, false, false);  // steps-2, steps-1
 #undef CDC_SCAN_PAIR
+        // This span's carry-in bytes and identity, then the next span's prefetch.
+        const uint64_t g_cur = g, off_cur = off;
+        const uint32_t wb_cur = wb;
+        const uint8_t *base_cur = base;
+        g = next_full(g + gstride, si, off);
+        if (g < st.total_spans) prefetch();
         // Fix-up: re-test the first 48 positions with the true carry-in.
-        const uint64_t gw = lane < 48 ? L.tab[wb * kCopies + (lane & 31)] : 0;
+        const uint64_t gw = lane < 48 ? L.tab[wb_cur * kCopies + (lane & 31)] : 0;
         const uint64_t hw = readlane_u64(gear_prefix(gw, lane), 47);  // hash of the 48 bytes before
-        h = wave_shr1(h, off != 0 ? hw : 0);
+        h = wave_shr1(h, off_cur != 0 ? hw : 0);
         {
             uint64_t h0 = h;
             append_hits(quarter<kAlign>(h, F0, tab, rep, fp) == 0, lo, h0, ne, E);
@@ -423,7 +488,7 @@ __global__ __launch_bounds__(kScanThreads, 1) void scan_kernel(const StreamTable
             h0 = h;
             append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, lo + 32, h0, ne, E);
         }
-        flush_span(g, base, (uint32_t)span, ne, E, tab, rep, fp, cand, lane);
+        flush_span(g_cur, base_cur, (uint32_t)span, ne, E, tab, rep, fp, cand, lane);
     }
 }
 
@@ -469,7 +534,7 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 }
 
 
-// ---- resolve ---------------------------------------------------------------
+// ---- resolve: exact steps --------------------------------------------------
 //
 // A chunk starting at s is cut at the first p in [s+a0, s+re) whose in-chunk
 // hash (reset at s+a0) hits mask_s below the centre or mask_l above it, else
@@ -478,66 +543,79 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 // <= 47 "truncated" positions s+a0 .. s+a0+46, which are tested exactly from
 // the bytes; every later position comes from the scan's records.
 
-constexpr int kResThreads = 256;      // 4 waves, one span (or one 64-span block) each
-constexpr int kResWaves = kResThreads / 64;
-constexpr uint32_t kMaxCap = 256;     // Engine clamps the record capacity to <= 256
-constexpr uint32_t kTruncMax = 47;    // mask bits <= 47 (checked on the host)
-constexpr uint32_t kNoRec = 0;        // window record index + 1; 0 = not a record
+constexpr int kResWaves = 4;
+constexpr int kResThreads = kResWaves * 64;
 
-struct Regime {
-    uint64_t rem, a0, ce, re, tl;
-};
-
-// Chunk regime at start s (SURVEY.md A.2): rem clipped to max, centre, and
-// the even-rounded scan bounds; tl = end of the truncated positions.
-__device__ __forceinline__ Regime regime(const FastParams &fp, uint64_t s, uint64_t n) {
-    Regime R;
-    uint64_t rem = n - s, center = fp.avg;
-    if (rem > fp.max) rem = fp.max; else if (rem < center) center = rem;
-    R.rem = rem;
-    R.a0 = (fp.min / 2) * 2;
-    R.ce = (center / 2) * 2;
-    R.re = (rem / 2) * 2;
-    R.tl = min(R.a0 + (uint64_t)fp.trunc, R.re);
-    return R;
-}
-
-// Dword at byte offset `off` (4-aligned) of a stream of n bytes, zero past n.
-__device__ __forceinline__ uint32_t ld4_guarded(const uint8_t *data, uint64_t off, uint64_t n) {
-    if (off + 4 <= n) return *(g_u32 *)(data + off);
-    uint32_t w = 0;
-    g_u8 *gb = as_global1(data);
-    for (uint64_t j = 0; off + j < n; ++j) w |= (uint32_t)gb[off + j] << (8 * j);
-    return w;
-}
+typedef const __attribute__((address_space(3))) uint64_t lds_u64;
 
 // First hitting offset d in [0, tl-a0) of the truncated positions of the
-// chunk starting at s, or ~0u.  Lane-level: the <= 52 bytes are staged in
-// this thread's 13-dword LDS slot `wl`, then a predicated 47-step chain.
-__device__ __forceinline__ uint32_t trunc_first(const uint8_t *data, uint64_t n, uint64_t s, const Regime &R,
-                                                const FastParams &fp, const uint64_t *tab, uint32_t *wl) {
-    const uint64_t w0 = s + R.a0, al = w0 & ~3ull;
-    const uint32_t len = (uint32_t)(R.tl - R.a0);
+// chunk starting at c (hash reset at c+a0), or kTruncNone; w0 = c + a0.
+// Lane-level: the <= 52 bytes arrive as 13 dword loads, are realigned in
+// registers with v_alignbyte_b32, and all 47 GEAR lookups are independent of
+// the chain, so the LDS latency is paid about once.  Needs al + 52 <= n.
+__device__ __forceinline__ uint32_t trunc_words(const uint8_t *data, uint64_t w0, uint32_t len, uint64_t a0,
+                                                uint64_t ce, uint64_t mask_s, uint64_t mask_l, lds_u64 *tab) {
+    const uint64_t al = w0 & ~3ull;
+    const uint32_t sh = (uint32_t)(w0 - al);
     uint32_t w[13];
-    if (al + 52 <= n) {
 #pragma unroll
-        for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(data + al + 4 * i);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 13; ++i) w[i] = ld4_guarded(data, al + 4 * i, n);
-    }
-#pragma unroll
-    for (int i = 0; i < 13; ++i) wl[i] = w[i];
-    const uint8_t *bytes = reinterpret_cast<const uint8_t *>(wl) + (w0 - al);
+    for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(data + al + 4 * i);
     uint64_t h = 0;
-    uint32_t t = ~0u;
-#pragma unroll 8
-    for (uint32_t d = 0; d < kTruncMax; ++d) {  // no early exit: the LDS reads pipeline
-        h = shl1_add(h, tab[bytes[d]]);
-        const bool hit = d < len && !(h & ((R.a0 + d) < R.ce ? fp.mask_s : fp.mask_l));
-        t = hit ? min(t, d) : t;
+    uint32_t t = kTruncNone;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const uint32_t a = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);  // bytes w0+4k .. w0+4k+3
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t d = 4 * k + j;
+            if (d >= kTruncMax) break;
+            h = shl1_add(h, tab[(a >> (8 * j)) & 255]);
+            const bool hit = d < len && !(h & ((a0 + d) < ce ? mask_s : mask_l));
+            t = (hit && t == kTruncNone) ? d : t;
+        }
     }
     return t;
+}
+
+// The same for any chunk start, out of line: every rare caller (virtual
+// entries, exact walk steps, the dense path) shares this one copy, which
+// keeps the resolve kernel's code inside the instruction cache.  Near the
+// end of the stream the bytes are read one at a time (positions >= n are
+// never tested: d < len).
+__device__ __noinline__ uint32_t trunc_at(const uint8_t *data, uint64_t n, uint64_t c, uint64_t mask_s,
+                                          uint64_t mask_l, uint32_t mn, uint32_t avg, uint32_t mx, uint32_t trunc,
+                                          lds_u64 *tab) {
+    if (n - c <= mn) return kTruncNone;
+    uint64_t rem = n - c, center = avg;
+    if (rem > mx) rem = mx; else if (rem < center) center = rem;
+    const uint64_t a0 = (mn / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
+    const uint64_t tl = min(a0 + (uint64_t)trunc, re);
+    if (tl <= a0) return kTruncNone;
+    const uint32_t len = (uint32_t)(tl - a0);
+    const uint64_t w0 = c + a0;
+    if ((w0 & ~3ull) + 52 <= n) return trunc_words(data, w0, len, a0, ce, mask_s, mask_l, tab);
+    uint64_t h = 0;
+    for (uint32_t d = 0; d < len; ++d) {
+        h = (h << 1) + tab[as_global1(data)[w0 + d]];
+        if (!(h & ((a0 + d) < ce ? mask_s : mask_l))) return d;
+    }
+    return kTruncNone;
+}
+
+__device__ __forceinline__ uint32_t trunc_call(const uint8_t *data, uint64_t n, uint64_t c, const FastParams &fp,
+                                               const uint64_t *tab) {
+    return trunc_at(data, n, c, fp.mask_s, fp.mask_l, fp.min, fp.avg, fp.max, fp.trunc, (lds_u64 *)tab);
+}
+
+// Inlined form for the per-record batch (the hot caller).
+__device__ __forceinline__ uint32_t trunc_bytes(const uint8_t *data, uint64_t n, uint64_t c, const FastParams &fp,
+                                                const uint64_t *tab) {
+    if (n - c <= fp.min) return kTruncNone;
+    const Regime R = regime(fp, c, n);
+    if (R.tl <= R.a0) return kTruncNone;
+    const uint64_t w0 = c + R.a0;
+    if ((w0 & ~3ull) + 52 > n) return trunc_call(data, n, c, fp, tab);
+    return trunc_words(data, w0, (uint32_t)(R.tl - R.a0), R.a0, R.ce, fp.mask_s, fp.mask_l, (lds_u64 *)tab);
 }
 
 // Exact next start from the bytes alone, wave-cooperative (64 positions per
@@ -562,203 +640,6 @@ __device__ __noinline__ uint64_t coop_next_bytes(const FastParams fp, const uint
     return s + R.rem;
 }
 
-// Per-wave LDS of the chain walk: the records of spans g-1, g, g+1 (window
-// slots 0, 1, 2; in position order slot by slot) and the links of the
-// records of slots 0 and 1.
-struct WaveWin {
-    uint32_t rec[3 * kMaxCap];
-    uint32_t link[2 * kMaxCap];   // next start - record position (<= max <= 16 MiB)
-    uint16_t lrec[2 * kMaxCap];   // window record index + 1 of the next start, 0: none
-    uint16_t lok[2 * kMaxCap];    // 1: link computed
-};
-
-struct SpanCtx {
-    uint64_t g, off, n, span, span_end;
-    uint32_t si, cap;
-    const uint8_t *data;
-    uint32_t cnt[3];    // records per slot (0 when the slot is outside the stream)
-    uint64_t soff[3];   // stream offset of each slot's span
-    bool ovf;           // a needed record list overflowed
-};
-
-__device__ __forceinline__ uint64_t win_pos(const SpanCtx &C, const WaveWin &W, uint32_t w) {
-    const uint32_t slot = w / C.cap;
-    return C.soff[slot] + (W.rec[w] & kCandPosMask);
-}
-
-// Window index + 1 of the record at stream offset p, 0 if none (binary
-// search per slot; records are position-sorted).
-__device__ __forceinline__ uint32_t win_lookup(const SpanCtx &C, const WaveWin &W, uint64_t p) {
-#pragma unroll
-    for (uint32_t slot = 0; slot < 3; ++slot) {
-        if (p < C.soff[slot] || p >= C.soff[slot] + C.span || C.cnt[slot] == 0) continue;
-        const uint32_t rel = (uint32_t)(p - C.soff[slot]);
-        const uint32_t *P = W.rec + slot * C.cap;
-        uint32_t a = 0, b = C.cnt[slot];
-        while (a < b) {
-            const uint32_t m = (a + b) >> 1;
-            if ((P[m] & kCandPosMask) < rel) a = m + 1; else b = m;
-        }
-        if (a < C.cnt[slot] && (P[a] & kCandPosMask) == rel) return slot * C.cap + a + 1;
-        return kNoRec;
-    }
-    return kNoRec;
-}
-
-// First window index whose record position is >= p (3*cap if none).
-__device__ __forceinline__ uint32_t win_first_from(const SpanCtx &C, const WaveWin &W, uint64_t p) {
-    for (uint32_t slot = 0; slot < 3; ++slot) {
-        if (p >= C.soff[slot] + C.span) continue;  // (slot 0 at off 0 wraps to 0: skipped)
-        const uint32_t rel = p > C.soff[slot] ? (uint32_t)(p - C.soff[slot]) : 0u;
-        const uint32_t *P = W.rec + slot * C.cap;
-        uint32_t a = 0, b = C.cnt[slot];
-        while (a < b) {
-            const uint32_t m = (a + b) >> 1;
-            if ((P[m] & kCandPosMask) < rel) a = m + 1; else b = m;
-        }
-        if (a < C.cnt[slot]) return slot * C.cap + a;
-    }
-    return 3 * C.cap;
-}
-
-// Next start after a chunk starting at s, lane-level, from the truncated
-// bytes and the window records.  *wr = window index + 1 of the result when it
-// is a record.  `first_w` = the first window index whose record position is
-// >= s (search starts there).
-__device__ uint64_t lane_next(const SpanCtx &C, const WaveWin &W, const FastParams &fp, const uint64_t *tab,
-                              uint32_t *wl, uint64_t s, uint32_t first_w, uint32_t *wr) {
-    *wr = kNoRec;
-    if (C.n - s <= fp.min) return C.n;  // tail chunk
-    const Regime R = regime(fp, s, C.n);
-    uint64_t nx = s + R.rem;
-    bool found = false;
-    if (R.tl > R.a0) {
-        const uint32_t t = trunc_first(C.data, C.n, s, R, fp, tab, wl);
-        if (t != ~0u) {
-            nx = s + R.a0 + t;
-            found = true;
-        }
-    }
-    if (!found && R.tl < R.re) {
-        const uint64_t lo = s + R.tl, hi = s + R.re;
-        for (uint32_t slot = first_w / C.cap; slot < 3 && !found; ++slot) {
-            const uint32_t k0 = slot == first_w / C.cap ? first_w % C.cap : 0;
-            for (uint32_t k = k0; k < C.cnt[slot]; ++k) {
-                const uint32_t r = W.rec[slot * C.cap + k];
-                const uint64_t c = C.soff[slot] + (r & kCandPosMask);
-                if (c >= hi) {
-                    found = true;  // no qualifying record: cut at max / end
-                    break;
-                }
-                if (c < lo) continue;
-                if (r & ((c - s) < R.ce ? kCandHitS : kCandHitL)) {
-                    nx = c;
-                    *wr = slot * C.cap + k + 1;
-                    found = true;
-                    break;
-                }
-            }
-        }
-    }
-    if (*wr == kNoRec && nx < C.span_end) *wr = win_lookup(C, W, nx);
-    return nx;
-}
-
-// Load the window (slots of spans g-1 .. g+1 that lie in g's stream).
-__device__ void load_window(SpanCtx &C, WaveWin &W, const StreamTable &st, const Candidates &cand,
-                            bool need_prev, uint32_t lane) {
-    C.ovf = false;
-#pragma unroll
-    for (int slot = 0; slot < 3; ++slot) {
-        C.cnt[slot] = 0;
-        C.soff[slot] = C.off + (uint64_t)slot * C.span - C.span;  // wraps for slot 0 at off 0: unused then
-        const bool in = slot == 1 || (slot == 0 && need_prev && C.off != 0) ||
-                        (slot == 2 && C.off + C.span < C.n);
-        if (!in) continue;
-        const uint64_t gs = C.g + slot - 1;
-        const uint32_t c = cand.count[gs];
-        if (c > cand.cap) {
-            C.ovf = true;
-            continue;
-        }
-        C.cnt[slot] = c;
-        for (uint32_t k = lane; k < c; k += 64) W.rec[slot * C.cap + k] = cand.pos[gs * cand.cap + k];
-    }
-    wave_sync_lds();
-}
-
-// Walk span g's chain from start w0 (a true start when `exact`, else a
-// warm-up guess): links of every record in [w0, span_end) lane-parallel,
-// then the walk.  Writes the span's starts; returns (cnt, entry, exit).
-__device__ void walk_span(SpanCtx &C, WaveWin &W, const FastParams &fp, const uint64_t *tab, uint32_t *wl,
-                          const Chains &ch, uint64_t w0, uint32_t lane, uint32_t &cnt_out, uint64_t &entry,
-                          uint64_t &exit) {
-    uint64_t *list = ch.starts + C.g * ch.smax;
-    uint32_t cnt = 0;
-    uint64_t s = w0;
-    entry = ~0ull;
-    if (C.ovf) {
-        // Exact byte-level walk (degenerate data: a record list overflowed).
-        while (s < C.span_end) {
-            if (s >= C.off) {
-                if (cnt < ch.smax && lane == 0) list[cnt] = s;
-                if (cnt == 0) entry = s;
-                ++cnt;
-            }
-            s = coop_next_bytes(fp, tab, C.data, C.n, s, lane);
-        }
-    } else {
-        // 1. Links for every record in [w0, span_end): lane per record.
-        const uint32_t nw = C.cap + C.cnt[1];  // slots 0 and 1 (slot 0 padded to cap)
-        for (uint32_t w = lane; w < 2 * C.cap; w += 64) W.lok[w] = 0;
-        wave_sync_lds();
-        for (uint32_t w = lane; w < nw; w += 64) {
-            bool act = w < nw && (w >= C.cap || w < C.cnt[0]);
-            uint64_t c = 0;
-            if (act) {
-                c = win_pos(C, W, w);
-                act = c >= w0 && c < C.span_end;
-            }
-            if (act) {
-                uint32_t wr;
-                const uint64_t nx = lane_next(C, W, fp, tab, wl, c, w + 1, &wr);
-                W.link[w] = (uint32_t)(nx - c);
-                W.lrec[w] = (uint16_t)wr;
-                W.lok[w] = 1;
-            }
-        }
-        wave_sync_lds();
-        // 2. The walk (wave-uniform): links where the start is a record,
-        //    lane 0 computes the rare other steps (after a max cut or a
-        //    truncated hit) and broadcasts them.
-        uint32_t wr = win_lookup(C, W, s);
-        while (s < C.span_end) {
-            if (s >= C.off) {
-                if (cnt < ch.smax && lane == 0) list[cnt] = s;
-                if (cnt == 0) entry = s;
-                ++cnt;
-            }
-            if (wr != kNoRec && wr - 1 < 2 * C.cap && W.lok[wr - 1]) {
-                const uint32_t k = wr - 1;
-                s += W.link[k];
-                wr = W.lrec[k];
-            } else {
-                uint64_t nx = 0;
-                uint32_t nwr = 0;
-                if (lane == 0) {
-                    const uint32_t fw = win_first_from(C, W, s);
-                    nx = lane_next(C, W, fp, tab, wl, s, fw, &nwr);
-                }
-                s = readlane_u64(nx, 0);
-                wr = (uint32_t)__builtin_amdgcn_readlane((int)nwr, 0);
-            }
-        }
-    }
-    if (cnt == 0) entry = s;
-    cnt_out = cnt;
-    exit = s;
-}
-
 __device__ __forceinline__ void load_tab1(uint64_t *tab, const uint64_t *gear) {
     for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = gear[i];
     __syncthreads();
@@ -770,234 +651,759 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
     return v;
 }
 
-__device__ __forceinline__ void span_ctx(SpanCtx &C, const StreamTable &st, const Candidates &cand, uint64_t g) {
-    C.g = g;
-    locate(st, g, C.si, C.off);
-    C.n = st.lens[C.si];
-    C.data = st.ptrs[C.si];
-    C.span = 1ull << st.span_log2;
-    C.span_end = min(C.off + C.span, C.n);
-    C.cap = cand.cap;
-}
-
-// Speculative chain of every span from a warm-up start before it (exact when
-// that start is the stream start).
-__global__ __launch_bounds__(kResThreads) void chain_kernel(const StreamTable st, const FastParams fp,
-                                                            const uint64_t *__restrict__ gear,
-                                                            const Candidates cand, const Chains ch,
-                                                            const Compact cp) {
-    __shared__ uint64_t tab[256];
-    __shared__ WaveWin win[kResWaves];
-    __shared__ uint32_t tw[kResThreads * 13];
-    load_tab1(tab, gear);
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t g = (uint64_t)blockIdx.x * kResWaves + wave;
-    if (g >= st.total_spans) return;  // no block-level barrier below
-    SpanCtx C;
-    span_ctx(C, st, cand, g);
-    const uint64_t warm = min(2ull * fp.max, C.span);
-    const uint64_t w0 = C.off > warm ? C.off - warm : 0;
-    load_window(C, win[wave], st, cand, w0 < C.off, lane);
-    uint32_t cnt;
-    uint64_t entry, exit;
-    walk_span(C, win[wave], fp, tab, tw + threadIdx.x * 13, ch, w0, lane, cnt, entry, exit);
-    if (lane == 0) {
-        ch.nst[g] = cnt;
-        ch.ent[g] = entry;
-        ch.ex[g] = exit;
-        if ((g & 63) == 63 || g + 1 == st.total_spans) ch.bx[0][g >> 6] = exit;
-        const uint32_t kc = cand.count[g];
-        if (kc <= cand.cap) atomicAdd((unsigned long long *)&cp.stats[kStatCand], (unsigned long long)kc);
-        else atomicAdd((unsigned long long *)&cp.stats[kStatOvf], 1ull);
-        if (cnt > ch.smax) atomicAdd((unsigned long long *)&cp.stats[kStatError], 1ull);
-    }
-}
-
-// Sequentially settle one 64-span block b: re-walk, in span order, every span
-// whose entry differs from its predecessor's exit.  Lane 0's predecessor exit
-// is `pred0` (valid when has_pred0).  Returns the block's last exit.
-__device__ uint64_t settle_block(const StreamTable &st, const FastParams &fp, const uint64_t *tab, uint32_t *wl,
-                                 const Candidates &cand, const Chains &ch, WaveWin &W, uint64_t b, bool has_pred0,
-                                 uint64_t pred0, uint32_t lane, uint64_t &rewalks, uint64_t &errs) {
-    const uint64_t g = b * 64 + lane;
-    const bool valid = g < st.total_spans;
-    uint64_t off = 0, E = 0, X = 0;
-    uint32_t si = 0;
-    if (valid) {
-        locate(st, g, si, off);
-        E = ch.ent[g];
-        X = ch.ex[g];
-    }
-    const bool first = off == 0;
-    uint64_t pred = __shfl_up(X, 1);
-    if (lane == 0) pred = pred0;
-    bool mism = valid && !first && (lane > 0 || has_pred0) && E != pred;
-    for (uint64_t m = __ballot(mism); m; m = __ballot(mism)) {
-        const int l0 = __ffsll((long long)m) - 1;
-        const uint64_t e = readlane_u64(pred, l0);
-        SpanCtx C;
-        span_ctx(C, st, cand, b * 64 + l0);
-        load_window(C, W, st, cand, false, lane);
-        uint32_t cnt;
-        uint64_t entry, exit;
-        walk_span(C, W, fp, tab, wl, ch, e, lane, cnt, entry, exit);
-        if (lane == 0) {
-            ch.nst[C.g] = cnt;
-            ch.ent[C.g] = entry;
-            ch.ex[C.g] = exit;
-            if (cnt > ch.smax) ++errs;
+// Next start after a chunk starting at s, lane-level, from the bytes of the
+// truncated positions and a binary search in the global record lists
+// (gbase: the stream's first span).  Returns ~0ull when a record list it
+// needs overflowed (the caller then uses coop_next_bytes).
+__device__ __forceinline__ uint64_t lane_next_global(const StreamTable &st, const FastParams &fp,
+                                                     const Candidates &cand, const uint64_t *tab,
+                                                     const uint8_t *data, uint64_t n, uint64_t gbase, uint64_t s) {
+    if (n - s <= fp.min) return n;
+    const Regime R = regime(fp, s, n);
+    const uint32_t t = trunc_call(data, n, s, fp, tab);
+    if (t != kTruncNone) return s + R.a0 + t;
+    if (R.tl >= R.re) return s + R.rem;
+    const uint64_t lo = s + R.tl, hi = s + R.re;
+    for (uint64_t sp = lo >> st.span_log2; (sp << st.span_log2) < hi; ++sp) {
+        const uint64_t g = gbase + sp;
+        const uint32_t cnt = cand.count[g];
+        if (cnt > cand.cap) return ~0ull;
+        const uint32_t *P = cand.pos + g * cand.cap;
+        const uint64_t sp0 = sp << st.span_log2;
+        const uint32_t lo_rel = lo > sp0 ? (uint32_t)(lo - sp0) : 0u;
+        uint32_t a = 0, b = cnt;  // first record at or after lo
+        while (a < b) {
+            const uint32_t m = (a + b) >> 1;
+            if ((P[m] & kCandPosMask) < lo_rel) a = m + 1; else b = m;
         }
-        ++rewalks;
-        if ((int)lane == l0) {
-            mism = false;
-            X = exit;
-        }
-        if ((int)lane == l0 + 1 && valid && !first) {
-            pred = exit;
-            mism = E != exit;
+        for (uint32_t j = a; j < cnt; ++j) {
+            const uint32_t r = P[j];
+            const uint64_t c = sp0 + (r & kCandPosMask);
+            if (c >= hi) return s + R.rem;
+            if (r & ((c - s) < R.ce ? kCandHitS : kCandHitL)) return c;
         }
     }
-    const int last = (int)min((uint64_t)63, st.total_spans - 1 - b * 64);
-    return readlane_u64(X, last);
+    return s + R.rem;
 }
 
-// One Jacobi pass: wave per 64-span block; lane 0's predecessor is the
-// previous block's last exit as of the previous pass (bx[pass&1]); this
-// pass's block exits go to bx[(pass+1)&1].  A pass after a pass that changed
-// no block exit has nothing to do and returns at once.
-__global__ __launch_bounds__(kResThreads) void fix_kernel(const StreamTable st, const FastParams fp,
-                                                          const uint64_t *__restrict__ gear,
-                                                          const Candidates cand, const Chains ch,
-                                                          const Compact cp, int pass) {
-    __shared__ uint64_t tab[256];
-    __shared__ WaveWin win[kResWaves];
-    __shared__ uint32_t tw[kResThreads * 13];
-    if (pass > 0 && __hip_atomic_load(&cp.stats[kStatFlag0 + pass - 1], __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT) == 0)
-        return;  // converged (uniform across the grid)
-    load_tab1(tab, gear);
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t b = (uint64_t)blockIdx.x * kResWaves + wave;
-    const uint64_t nblocks = (st.total_spans + 63) / 64;
-    if (b >= nblocks) return;
-    uint64_t rewalks = 0, errs = 0;
-    const uint64_t pred0 = b > 0 ? ch.bx[pass & 1][b - 1] : 0;
-    const uint64_t last = settle_block(st, fp, tab, tw + threadIdx.x * 13, cand, ch, win[wave], b, b > 0, pred0,
-                                       lane, rewalks, errs);
-    if (lane == 0) {
-        ch.bx[(pass + 1) & 1][b] = last;
-        if (last != ch.bx[pass & 1][b])
-            __hip_atomic_store(&cp.stats[kStatFlag0 + pass], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (rewalks) atomicAdd((unsigned long long *)&cp.stats[kStatRewalk], (unsigned long long)rewalks);
-        if (errs) atomicAdd((unsigned long long *)&cp.stats[kStatError], (unsigned long long)errs);
-    }
-}
+struct LaneSpan {
+    bool act, first;
+    uint32_t si;
+    uint64_t g, off, span_end, n, gbase;
+    const uint8_t *data;
+};
 
-// Runs only when the last Jacobi pass still changed a block exit (degenerate
-// data whose chains never merge): one wave settles every block in order.
-__global__ __launch_bounds__(64) void serial_kernel(const StreamTable st, const FastParams fp,
-                                                    const uint64_t *__restrict__ gear, const Candidates cand,
-                                                    const Chains ch, const Compact cp) {
-    __shared__ uint64_t tab[256];
-    __shared__ WaveWin win;
-    __shared__ uint32_t tw[64 * 13];
-    if (__hip_atomic_load(&cp.stats[kStatFlag0 + kPasses - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-        return;
-    load_tab1(tab, gear);
-    const uint32_t lane = threadIdx.x;
-    const uint64_t nblocks = (st.total_spans + 63) / 64;
-    uint64_t rewalks = 0, errs = 0, pred0 = 0;
-    for (uint64_t b = 0; b < nblocks; ++b)
-        pred0 = settle_block(st, fp, tab, tw + lane * 13, cand, ch, win, b, b > 0, pred0, lane, rewalks, errs);
-    if (lane == 0) {
-        cp.stats[kStatSerial] = 1;
-        cp.stats[kStatRewalk] += rewalks;
-        cp.stats[kStatError] += errs;
-    }
-}
-
-constexpr int kCompThreads = 1024;
-
-__device__ __forceinline__ uint64_t block_sum_1024(uint64_t v, uint64_t *red) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    v = wave_sum(v);
-    if (lane == 0) red[wave] = v;
-    __syncthreads();
-    uint64_t t = lane < kCompThreads / 64 ? red[lane] : 0;
-    t = wave_sum(t);
-    __syncthreads();
-    return t;
-}
-
-// Chunk count per 1024-span block.
-__global__ __launch_bounds__(kCompThreads) void count_kernel(const StreamTable st, const Chains ch,
-                                                             const Compact cp) {
-    __shared__ uint64_t red[kCompThreads / 64];
-    const uint64_t g = (uint64_t)blockIdx.x * kCompThreads + threadIdx.x;
-    const uint64_t v = g < st.total_spans ? min(ch.nst[g], ch.smax) : 0;
-    const uint64_t t = block_sum_1024(v, red);
-    if (threadIdx.x == 0) cp.bsum[blockIdx.x] = t;
-}
-
-// Output: span g's chunks at their final index; first[] and the statistics
-// straight into host-coherent memory (the last block copies the stats).
-__global__ __launch_bounds__(kCompThreads) void write_kernel(const StreamTable st, const Chains ch,
-                                                             const Compact cp, cdc_chunk_pod *out,
-                                                             uint64_t out_cap) {
-    __shared__ uint64_t red[kCompThreads / 64];
-    __shared__ uint64_t wex[kCompThreads / 64];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t pre = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kCompThreads) pre += cp.bsum[b];
-    const uint64_t base = block_sum_1024(pre, red);
-    const uint64_t g = (uint64_t)blockIdx.x * kCompThreads + threadIdx.x;
-    const bool valid = g < st.total_spans;
-    const uint32_t cnt = valid ? ch.nst[g] : 0;
-    const uint32_t c = min(cnt, ch.smax);
-    // exclusive scan of c over the block
-    uint64_t x = c;
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) {
-        const uint64_t t = __shfl_up(x, k);
-        if (lane >= (uint32_t)k) x += t;
-    }
-    if (lane == 63) wex[wave] = x;
-    __syncthreads();
-    uint64_t wbase = 0;
-    for (uint32_t w = 0; w < wave; ++w) wbase += wex[w];
-    const uint64_t idx = base + wbase + x - c;
-    uint64_t err = 0;
-    if (valid) {
-        uint32_t si;
-        uint64_t off;
-        locate(st, g, si, off);
-        if (cnt > ch.smax || idx + c > out_cap) {
-            err = 1;  // impossible for a consistent chain: report, never write out of bounds
-        } else {
-            const uint64_t *list = ch.starts + g * ch.smax;
-            const uint64_t exit = ch.ex[g];
-            for (uint32_t k = 0; k < c; ++k) {
-                const uint64_t s0 = list[k];
-                const uint64_t nx = k + 1 < c ? list[k + 1] : exit;
-                out[idx + k] = cdc_chunk_pod{s0, nx - s0};
+// Walk every lane with go=true from s to its span's end, exact, from the
+// bytes and the global record lists (lane_next_global; across an overflowed
+// record list the whole wave steps with coop_next_bytes).  For windows too
+// dense for the LDS path.  Writes the starts >= off to the span's list.
+// Wave-synchronous.
+__device__ __forceinline__ void walk_lanes(const StreamTable &st, const FastParams &fp, const Candidates &cand,
+                                           const uint64_t *tab, const Chains &ch, const LaneSpan &L,
+                                           uint32_t lane, bool go, uint64_t s, uint32_t &cnt, uint64_t &entry,
+                                           uint64_t &exit, uint64_t &steps) {
+    uint64_t *list = ch.starts + L.g * ch.smax;
+    cnt = 0;
+    entry = ~0ull;
+    go = go && s < L.span_end;
+    for (;;) {
+        bool need = false;
+        if (go) {
+            if (s >= L.off) {
+                if (cnt < ch.smax) list[cnt] = s;
+                if (cnt == 0) entry = s;
+                ++cnt;
+            }
+            ++steps;
+            const uint64_t nx = lane_next_global(st, fp, cand, tab, L.data, L.n, L.gbase, s);
+            if (nx == ~0ull) need = true; else s = nx;
+            go = !need && s < L.span_end;
+        }
+        for (uint64_t m = __ballot(need); m; m &= m - 1) {
+            const int l = __ffsll((long long)m) - 1;
+            const uint64_t sl = readlane_u64(s, l), nl = readlane_u64(L.n, l);
+            const uint8_t *dl = reinterpret_cast<const uint8_t *>(readlane_u64(reinterpret_cast<uint64_t>(L.data), l));
+            const uint64_t nx = coop_next_bytes(fp, tab, dl, nl, sl, lane);
+            if ((int)lane == l) {
+                s = nx;
+                go = s < L.span_end;
             }
         }
-        if (off == 0) cp.h_first[si] = idx;
-        if (g + 1 == st.total_spans) cp.h_first[st.n] = idx + c;
+        if (__ballot(go) == 0) break;
     }
-    err = block_sum_1024(err, red);
+    if (cnt == 0) entry = s;
+    exit = s;
+}
+
+// ---- resolve: window, links, walks, look-back --------------------------------
+//
+// One block = kResWaves waves = kBlockSpans consecutive spans.  Wave w walks
+// kWalkSpans of them (lane l: span G0 + l), each from a warm-up start
+// kWarmSpans spans back, over links held in a compact per-wave LDS window:
+//   1. window metadata and every record of the window's kWinSlots spans, one
+//      batch of global loads;
+//   2. the truncated-region result of every record in reach (lane per record);
+//   3. the link of every record in reach -- the next chunk start after a chunk
+//      starting there -- lane per record, an LDS search.  Next starts that
+//      are not records (max cuts, truncated hits) become "virtual" entries,
+//      whose links are computed the same way from the bytes until none is new;
+//   4. the walks: LDS pointer chasing; the spans' chunk starts go to HBM;
+//   5. block settle: a span whose entry differs from its predecessor's exit
+//      is re-walked from that exit (rare; in order);
+//   6. decoupled look-back over blocks in dispatch order: the chunk-count
+//      prefix and the block-boundary check (this block's entry == the
+//      predecessor's exit).  A failed check waits for the block at fault to
+//      publish its final state; a block whose own entry is stale re-walks;
+//   7. Chunk{offset,length} at the final index, first[] and the statistics.
+constexpr int kWalkSpans = 8;
+constexpr int kWarmSpans = 2;
+constexpr int kWinSlots = kWarmSpans + kWalkSpans + 1;  // + 1: searched, never walked
+constexpr int kReach = kWarmSpans + kWalkSpans;         // slots whose records get links
+constexpr uint32_t kWinRecs = 768;  // per-wave record budget (denser windows: global path)
+constexpr uint32_t kVirt = 128;     // virtual entries per wave
+constexpr int kBlockSpans = kResWaves * kWalkSpans;
+constexpr uint64_t kNoDep = ~0ull;  // block entry of a block that starts a stream
+constexpr uint64_t kAgg = 1, kInc = 2;
+constexpr uint32_t kSpinMax = 1u << 26;  // look-back poll bound: an error, never a hang
+
+struct ChainWin {
+    uint32_t rec[kWinRecs];           // the window's records, slot after slot
+    uint32_t link[kWinRecs + kVirt];  // next start - entry position (0: not computed)
+    uint16_t lrec[kWinRecs + kVirt];  // entry index + 1 of that next start (0: not an entry)
+    uint8_t tr[kWinRecs];             // truncated-region result of each record in reach
+    uint8_t vslot[kVirt];             // virtual entries: slot, stream offset
+    uint64_t vpos[kVirt];
+    uint64_t soff[kWinSlots];         // stream offset of each slot's span
+    uint64_t slen[kWinSlots];         // its stream's length
+    const uint8_t *sptr[kWinSlots];   // its stream's bytes
+    uint32_t ssi[kWinSlots];          // its stream (~0u: no span)
+    uint32_t scnt[kWinSlots];         // its records (> cap: overflowed)
+    uint32_t pre[kWinSlots + 1];      // compact start of each slot's records
+    uint32_t wpre[kWalkSpans + 1];    // output: chunk prefix of the walked spans
+    uint32_t nvirt;
+};
+
+struct BlockState {
+    uint64_t E[kBlockSpans];  // entry: first start >= span start
+    uint64_t X[kBlockSpans];  // exit: first start >= span end
+    uint32_t N[kBlockSpans];  // starts in the span
+    uint8_t F[kBlockSpans];   // 1: the span starts a stream
+    uint64_t b, base, pred;
+    uint32_t rewalk;
+    uint64_t stat[kResWaves][3];  // per wave: candidates << 24 | overflowed, re-walks, exact steps
+    uint64_t diag[kResWaves][kStatDiagN];  // per wave phase times (diag & 128)
+};
+
+// Slot of window record i.
+__device__ __forceinline__ int win_slot(const ChainWin &W, uint32_t i) {
+    int j = 0;
+    while (j + 1 < kWinSlots && W.pre[j + 1] <= i) ++j;
+    return j;
+}
+
+// Local index of the first window record of stream si at or after p, or
+// kWinRecs when none.
+__device__ __forceinline__ uint32_t win_first_at(const ChainWin &W, uint32_t si, uint64_t p, uint64_t span) {
+#pragma unroll 1
+    for (int j = 0; j < kWinSlots; ++j) {
+        if (W.ssi[j] != si || W.soff[j] + span <= p) continue;
+        const uint32_t b0 = W.pre[j], b1 = W.pre[j + 1];
+        const uint32_t rel = p > W.soff[j] ? (uint32_t)(p - W.soff[j]) : 0u;
+        uint32_t a = b0, b = b1;
+        while (a < b) {
+            const uint32_t m = (a + b) >> 1;
+            if ((W.rec[m] & kCandPosMask) < rel) a = m + 1; else b = m;
+        }
+        if (a < b1) return a;
+    }
+    return kWinRecs;
+}
+
+// Entry index + 1 of a start exactly at p (a record or a virtual entry), or 0.
+__device__ __forceinline__ uint32_t win_entry_at(const ChainWin &W, uint32_t si, uint64_t p, uint64_t span) {
+    const uint32_t f = win_first_at(W, si, p, span);
+    if (f < kWinRecs && W.soff[win_slot(W, f)] + (W.rec[f] & kCandPosMask) == p) return f + 1;
+    for (uint32_t v = 0; v < W.nvirt; ++v)
+        if (W.vpos[v] == p && W.ssi[W.vslot[v]] == si) return kWinRecs + v + 1;
+    return 0;
+}
+
+// First qualifying window record for a chunk starting at c (stream si,
+// regime R): a linear scan from local index i0 (records are position-sorted
+// within a stream across consecutive slots).  Returns the position, or
+// c + rem when none is below c + re.  *lr = local index + 1.
+__device__ __forceinline__ uint64_t win_search(const ChainWin &W, uint32_t si, uint64_t c, const Regime &R,
+                                               uint32_t i0, uint32_t *lr) {
+    *lr = 0;
+    const uint64_t lo = c + R.tl, hi = c + R.re;
+    int j = 0;
+    for (uint32_t i = i0;; ++i) {
+        while (j < kWinSlots && i >= W.pre[j + 1]) ++j;
+        if (j >= kWinSlots || W.ssi[j] != si) break;
+        const uint32_t r = W.rec[i];
+        const uint64_t p = W.soff[j] + (r & kCandPosMask);
+        if (p >= hi) break;
+        if (p >= lo && (r & ((p - c) < R.ce ? kCandHitS : kCandHitL))) {
+            *lr = i + 1;
+            return p;
+        }
+    }
+    return c + R.rem;
+}
+
+// Next start after a chunk starting at c (stream si, n bytes): the truncated
+// result `tr` (or from the bytes when tr_known is false), else the first
+// qualifying window record from local index i0 on, else the max / end cut.
+// *lr = local index + 1 of the result when it is a window record.
+template <bool kTrKnown>
+__device__ __forceinline__ uint64_t win_next(const ChainWin &W, const FastParams &fp, const uint64_t *tab,
+                                             const uint8_t *data, uint64_t n, uint32_t si, uint64_t c,
+                                             uint32_t i0, uint32_t tr, uint32_t *lr) {
+    *lr = 0;
+    if (n - c <= fp.min) return n;  // tail chunk
+    const Regime R = regime(fp, c, n);
+    if (R.tl > R.a0) {
+        const uint32_t t = kTrKnown ? tr : trunc_call(data, n, c, fp, tab);
+        if (t != kTruncNone) return c + R.a0 + t;
+    }
+    if (R.tl >= R.re) return c + R.rem;
+    return win_search(W, si, c, R, i0, lr);
+}
+
+// Wave-uniform allocation of virtual entries: slot of this lane's new entry
+// (kVirt when the window's budget is spent); nv counts every request.
+__device__ __forceinline__ uint32_t virt_alloc(bool mk, uint32_t &nv) {
+    const uint64_t m = __ballot(mk);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const uint32_t v = nv + below;
+    nv += (uint32_t)__popcll(m);
+    return v < kVirt ? v : kVirt;
+}
+
+// Link of the chunk starting at c (window slot j) into W.link/W.lrec[e]; a
+// next start that is not a record but lies in a walked slot becomes a new
+// virtual entry.  Wave-synchronous (all lanes call; act = has an entry).
+template <bool kTrKnown>
+__device__ __forceinline__ void link_entry(ChainWin &W, const FastParams &fp, const uint64_t *tab, bool act,
+                                           uint32_t e, int j, uint64_t c, uint32_t i0, uint32_t tr, uint32_t sl2,
+                                           uint32_t &nv) {
+    bool mk = false;
+    uint64_t nx = 0;
+    uint32_t lr = 0;
+    int jt = 0;
+    if (act) {
+        const uint32_t si = W.ssi[j];
+        const uint64_t n = W.slen[j];
+        nx = win_next<kTrKnown>(W, fp, tab, W.sptr[j], n, si, c, i0, tr, &lr);
+        W.link[e] = (uint32_t)(nx - c);
+        jt = j + (int)((nx - W.soff[j]) >> sl2);  // <= j + 1: max <= span
+        mk = lr == 0 && nx < n && jt < kReach && W.ssi[jt] == si;
+    }
+    const uint32_t v = virt_alloc(mk, nv);
+    if (mk && v < kVirt) {
+        W.vpos[v] = nx;
+        W.vslot[v] = (uint8_t)jt;
+        lr = kWinRecs + v + 1;
+    }
+    if (act) W.lrec[e] = (uint16_t)lr;
+}
+
+// Walk every lane with go=true from s (entry index + 1 wr, 0: none) to its
+// span's end over the window links, writing the starts >= off to the span's
+// list.  A start without a link (a stream start, a spent virtual budget) takes
+// one exact step from the bytes.  Wave-synchronous.
+__device__ __forceinline__ void walk_window(const ChainWin &W, const FastParams &fp, const uint64_t *tab,
+                                            const LaneSpan &L, const Chains &ch, bool go, uint64_t s, uint32_t wr,
+                                            uint64_t span, uint32_t &cnt, uint64_t &entry, uint64_t &exit,
+                                            uint64_t &steps) {
+    uint64_t *list = ch.starts + L.g * ch.smax;
+    cnt = 0;
+    entry = ~0ull;
+    go = go && s < L.span_end;
+    for (;;) {
+        while (go) {
+            if (s >= L.off) {
+                if (cnt < ch.smax) list[cnt] = s;
+                if (cnt == 0) entry = s;
+                ++cnt;
+            }
+            if (wr == 0) break;
+            const uint32_t d = W.link[wr - 1];
+            if (d == 0) break;
+            wr = W.lrec[wr - 1];
+            s += d;
+            go = s < L.span_end;
+        }
+        if (!__ballot(go)) break;
+        if (go) {
+            ++steps;
+            uint32_t lr;
+            s = win_next<false>(W, fp, tab, L.data, L.n, L.si, s, win_first_at(W, L.si, s, span), 0, &lr);
+            wr = lr;
+            go = s < L.span_end;
+        }
+    }
+    if (cnt == 0) entry = s;
+    exit = s;
+}
+
+// Re-walk, in order, every span of this wave whose entry differs from its
+// predecessor's exit (lane 0's predecessor: pred0, when has0).  Lanes
+// 0..kWalkSpans-1 own the wave's spans B.*[k0 + lane].
+__device__ __forceinline__ void wave_settle(const StreamTable &st, const FastParams &fp, const Candidates &cand,
+                                            const uint64_t *tab, const Chains &ch, const ChainWin &W, bool dense,
+                                            const LaneSpan &L, uint32_t lane, uint32_t k0, bool has0,
+                                            uint64_t pred0, BlockState &B, uint64_t span, uint64_t &rewalks,
+                                            uint64_t &steps) {
+    const bool mine = lane < kWalkSpans && L.act;
+    uint64_t E = mine ? B.E[k0 + lane] : 0, X = mine ? B.X[k0 + lane] : 0;
+    for (;;) {
+        uint64_t pred = __shfl_up(X, 1);
+        if (lane == 0) pred = pred0;
+        const bool mism = mine && !L.first && (lane > 0 || has0) && E != pred;
+        const uint64_t m = __ballot(mism);
+        if (m == 0) break;
+        const bool ready = mism && !(lane > 0 && ((m >> (lane - 1)) & 1ull));  // predecessor settled
+        uint32_t cnt = 0;
+        uint64_t entry = 0, exit = 0;
+        if (dense)
+            walk_lanes(st, fp, cand, tab, ch, L, lane, ready, pred, cnt, entry, exit, steps);
+        else
+            walk_window(W, fp, tab, L, ch, ready, pred, ready ? win_entry_at(W, L.si, pred, span) : 0u, span, cnt,
+                        entry, exit, steps);
+        if (ready) {
+            B.E[k0 + lane] = E = entry;
+            B.X[k0 + lane] = X = exit;
+            B.N[k0 + lane] = cnt;
+            ++rewalks;
+        }
+    }
+}
+
+// Inter-block words (MI355X_MICROARCH.md "inter-workgroup visibility"; the
+// programming guide's Guideline 16 recipe R1): every descriptor word is
+// stored and loaded with agent-scope relaxed atomics (sc1: past the per-CU
+// L1 and the per-XCD L2), the payload drained before its status word.
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+    return __hip_atomic_load((g_u64 *)const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+    __hip_atomic_store((g_u64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void publish(const Resolve &rs, uint64_t b, uint64_t status, uint64_t cnt, uint64_t E,
+                                        uint64_t X, uint32_t lane) {
+    if (lane == 0) {
+        if (status == kAgg) {
+            st_agent(&rs.dagg[b], cnt);
+            st_agent(&rs.dE[b], E);
+            st_agent(&rs.dXa[b], X);
+        } else {
+            st_agent(&rs.dinc[b], cnt);
+            st_agent(&rs.dXi[b], X);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_agent(&rs.dstat[b], (rs.gen << 2) | status);
+    }
+}
+
+// Poll block j's status word until it is final (bounded: false on timeout).
+__device__ __forceinline__ bool wait_final(const Resolve &rs, uint64_t j) {
+    const uint64_t inc = (rs.gen << 2) | kInc;
+    for (uint32_t k = 0; k < kSpinMax; ++k) {
+        if (ld_agent(&rs.dstat[j]) == inc) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below)
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+
+// Exclusive chunk-count prefix of block b >= 1 (wave 0): walks back over the
+// predecessors' descriptors, 64 per step, to the nearest final (inclusive)
+// one, checking every block boundary on the way (exit of block j == entry of
+// block j+1, unless j+1 starts a stream).  Returns 1 with acc = the prefix
+// when this block's entry Eb holds; 0 with acc = the predecessor's inclusive
+// count and pred = its final exit when this block must re-walk from pred;
+// -1 on a poll timeout.
+__device__ int lookback(const Resolve &rs, uint64_t b, uint64_t Eb, uint32_t lane, uint64_t &acc, uint64_t &pred) {
+    const uint64_t agg_w = (rs.gen << 2) | kAgg, inc_w = (rs.gen << 2) | kInc;
+    for (uint32_t attempt = 0; attempt < 1024; ++attempt) {  // each retry follows a stale block going final
+        acc = 0;
+        uint64_t expect = Eb;  // entry of the block after this step's lane-0 block
+        int64_t j0 = (int64_t)b - 1;
+        int64_t stale = -1;
+        for (;;) {
+            const int64_t j = j0 - (int64_t)lane;
+            uint64_t w = j >= 0 ? 0 : inc_w;
+            uint64_t mi = 0;
+            uint32_t lim = 63;
+            for (uint32_t spins = 0;; ++spins) {
+                if (w != agg_w && w != inc_w) w = ld_agent(&rs.dstat[j]);
+                mi = __ballot(w == inc_w);
+                const uint64_t mp = __ballot(w == agg_w || w == inc_w);
+                lim = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63u;
+                const uint64_t need = lim == 63 ? ~0ull : (2ull << lim) - 1;
+                if ((mp & need) == need) break;
+                if (spins >= kSpinMax) return -1;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below)
+            const bool inc = w == inc_w;
+            uint64_t cnt = 0, E = kNoDep, X = 0;
+            if (j >= 0 && lane <= lim) {
+                cnt = ld_agent(inc ? &rs.dinc[j] : &rs.dagg[j]);
+                X = ld_agent(inc ? &rs.dXi[j] : &rs.dXa[j]);
+                if (!inc) E = ld_agent(&rs.dE[j]);
+            }
+            uint64_t En = __shfl_up(E, 1);
+            if (lane == 0) En = expect;
+            const uint64_t mb = __ballot(lane <= lim && En != kNoDep && X != En);
+            if (mb) {
+                stale = j0 - (int64_t)(__ffsll((long long)mb) - 1) + 1;  // the block whose entry is stale
+                break;
+            }
+            acc += wave_sum(lane <= lim ? cnt : 0);
+            if (mi) return 1;
+            expect = readlane_u64(E, 63);
+            j0 -= 64;
+        }
+        if (stale == (int64_t)b) {  // this block's own entry: the predecessor's final exit decides
+            if (!wait_final(rs, b - 1)) return -1;
+            acc = ld_agent(&rs.dinc[b - 1]);
+            pred = ld_agent(&rs.dXi[b - 1]);
+            return pred == Eb ? 1 : 0;
+        }
+        if (!wait_final(rs, (uint64_t)stale)) return -1;  // then look again
+    }
+    return -1;
+}
+
+// Chunk starts are re-read by the wave that stored them: nt loads (past L1).
+__device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) {
+    return __builtin_nontemporal_load((const g_u64 *)p);
+}
+
+// Phase timer (diag & 128): per-wave durations in registers, summed per block
+// at the end (one atomic per phase per block, not per wave).
+#define CDC_DIAG_T(k)                                                  \
+    do {                                                               \
+        if (fp.diag & 128) {                                           \
+            const uint64_t t_ = __builtin_amdgcn_s_memrealtime();       \
+            dt[k] += t_ - t_prev;                                      \
+            t_prev = t_;                                               \
+        }                                                              \
+    } while (0)
+
+// FastParams.diag (CHUNKFS_AMD_DIAG, read at cdc_create) -- test hooks and
+// timing experiments only, 0 in every real run: 1 = walks start at the span
+// start (no warm-up: nearly every boundary re-walks), 2 = every wave takes the
+// dense (global record list) path, 128 = phase timings into the stats.
+__global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable st, const FastParams fp,
+                                                              const uint64_t *__restrict__ gear,
+                                                              const Candidates cand, const Chains ch,
+                                                              const Compact cp, const Resolve rs,
+                                                              cdc_chunk_pod *out, uint64_t out_cap) {
+    __shared__ uint64_t tab[256];
+    __shared__ ChainWin win[kResWaves];
+    __shared__ BlockState B;
+    // Blocks take their index in dispatch order, so the look-back only ever
+    // waits on blocks that are already running or done.
     if (threadIdx.x == 0) {
+        B.b = atomicAdd((unsigned long long *)&cp.stats[kStatOrder], 1ull);
+        B.base = B.pred = 0;
+        B.rewalk = 0;
+    }
+    load_tab1(tab, gear);
+    const uint64_t b = B.b;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t sl2 = st.span_log2;
+    const uint64_t span = 1ull << sl2;
+    const uint64_t g0 = b * kBlockSpans;
+    const uint32_t nsp = (uint32_t)min((uint64_t)kBlockSpans, st.total_spans - g0);
+    const uint32_t k0 = wave * kWalkSpans;  // block index of this wave's first span
+    const uint64_t G0 = g0 + k0;
+    const uint32_t cap = cand.cap;
+    ChainWin &W = win[wave];
+    uint64_t t_prev = (fp.diag & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t dt[kStatDiagN] = {};
+    uint64_t steps = 0, rewalks = 0, cstat = 0;
+    LaneSpan L{};
+    bool dense = false;
+
+    if (k0 < nsp) {
+        const int64_t gfirst = (int64_t)G0 - kWarmSpans;  // span of slot 0
+        // 1. window metadata, then every record of the window (one batch of loads)
+        if (lane < kWinSlots) {
+            const int64_t g = gfirst + lane;
+            uint32_t si = ~0u, c = 0;
+            uint64_t off = 0, n = 0;
+            const uint8_t *p = nullptr;
+            if (g >= 0 && (uint64_t)g < st.total_spans) {
+                locate(st, (uint64_t)g, si, off);
+                c = cand.count[g];
+                n = st.lens[si];
+                p = st.ptrs[si];
+            }
+            W.ssi[lane] = si;
+            W.soff[lane] = off;
+            W.scnt[lane] = c;
+            W.slen[lane] = n;
+            W.sptr[lane] = p;
+        }
+        wave_sync_lds();
+        if (lane == 0) {
+            uint32_t acc = 0;
+            bool dn = (fp.diag & 2) != 0;
+#pragma unroll 1
+            for (int j = 0; j < kWinSlots; ++j) {
+                W.pre[j] = acc;
+                const uint32_t c = W.scnt[j];
+                if (c > cap) dn = true; else acc += c;
+            }
+            if (acc > kWinRecs) dn = true;
+            W.pre[kWinSlots] = dn ? 0 : acc;
+            W.nvirt = dn ? 1u : 0u;  // (the dense flag, for the other lanes)
+        }
+        wave_sync_lds();
+        dense = W.nvirt != 0;
+        if (lane < kWalkSpans && k0 + lane < nsp) {  // the walker's span: slot kWarmSpans + lane
+            const int j = kWarmSpans + (int)lane;
+            L.act = true;
+            L.g = G0 + lane;
+            L.si = W.ssi[j];
+            L.off = W.soff[j];
+            L.n = W.slen[j];
+            L.data = W.sptr[j];
+            L.gbase = L.g - (L.off >> sl2);
+            L.span_end = min(L.off + span, L.n);
+            L.first = L.off == 0;
+            const uint32_t c = W.scnt[j];
+            cstat = c > cap ? 1ull : (uint64_t)c << 24;
+        }
+        CDC_DIAG_T(0);
+        uint32_t cnt = 0;
+        uint64_t entry = 0, exit = 0;
+        if (dense) {
+            // Degenerate data: exact walks from the bytes and the global record lists.
+            uint64_t s0 = 0;
+            if (L.act && !L.first) s0 = L.off > kWarmSpans * span ? L.off - kWarmSpans * span : 0;
+            if (L.act && !L.first && (fp.diag & 1)) s0 = L.off;  // test hook: no warm-up
+            walk_lanes(st, fp, cand, tab, ch, L, lane, L.act, s0, cnt, entry, exit, steps);
+        } else {
+            const uint32_t nrec = W.pre[kWinSlots];
+            {
+                uint32_t v[kWinSlots];
+#pragma unroll
+                for (int j = 0; j < kWinSlots; ++j) {
+                    const uint32_t c = W.scnt[j];
+                    v[j] = cand.pos[lane < c ? (uint64_t)(gfirst + j) * cap + lane : 0];
+                }
+#pragma unroll
+                for (int j = 0; j < kWinSlots; ++j)
+                    if (lane < W.scnt[j]) W.rec[W.pre[j] + lane] = v[j];
+#pragma unroll 1
+                for (int j = 0; j < kWinSlots; ++j)  // slots with more than 64 records
+                    for (uint32_t k = lane + 64; k < W.scnt[j]; k += 64)
+                        W.rec[W.pre[j] + k] = cand.pos[(uint64_t)(gfirst + j) * cap + k];
+            }
+            wave_sync_lds();
+            CDC_DIAG_T(1);
+            // 2. truncated-region results of the records in reach
+            const uint32_t nlink = W.pre[kReach];
+            for (uint32_t i = lane; i < nlink; i += 64) {
+                const int j = win_slot(W, i);
+                W.tr[i] = (uint8_t)trunc_bytes(W.sptr[j], W.slen[j], W.soff[j] + (W.rec[i] & kCandPosMask), fp, tab);
+            }
+            for (uint32_t i = nlink + lane; i < nrec; i += 64) W.link[i] = 0;  // searched only
+            wave_sync_lds();
+            CDC_DIAG_T(2);
+            // 3. links: records in reach, then virtual entries until none is new
+            uint32_t nv = 0;
+            for (uint32_t base = 0; base < nlink; base += 64) {
+                const uint32_t i = base + lane;
+                const bool act = i < nlink;
+                const int j = act ? win_slot(W, i) : 0;
+                const uint64_t c = act ? W.soff[j] + (W.rec[i] & kCandPosMask) : 0;
+                link_entry<true>(W, fp, tab, act, i, j, c, i + 1, act ? W.tr[i] : 0u, sl2, nv);
+            }
+            wave_sync_lds();
+            CDC_DIAG_T(3);
+            for (uint32_t v0 = 0;;) {
+                const uint32_t v1 = min(nv, kVirt);
+                if (v0 >= v1) break;
+                for (uint32_t base = v0; base < v1; base += 64) {
+                    const uint32_t v = base + lane;
+                    const bool act = v < v1;
+                    const int j = act ? (int)W.vslot[v] : 0;
+                    const uint64_t c = act ? W.vpos[v] : 0;
+                    const uint32_t i0 = act ? win_first_at(W, W.ssi[j], c, span) : 0u;
+                    link_entry<false>(W, fp, tab, act, kWinRecs + v, j, c, i0, 0, sl2, nv);
+                }
+                wave_sync_lds();
+                v0 = v1;
+            }
+            if (lane == 0) W.nvirt = min(nv, kVirt);
+            wave_sync_lds();
+            CDC_DIAG_T(4);
+            // 4. the walks, from the first record kWarmSpans spans back (exact
+            // from a stream start)
+            uint64_t s = 0;
+            uint32_t wr = 0;
+            if (L.act && !L.first && L.off >= kWarmSpans * span) {
+                const int jw = (int)lane;  // slot of span g - kWarmSpans
+                if (W.pre[jw + 1] > W.pre[jw]) {
+                    wr = W.pre[jw] + 1;
+                    s = W.soff[jw] + (W.rec[W.pre[jw]] & kCandPosMask);
+                } else {
+                    s = W.soff[jw];
+                }
+            }
+            if (L.act && !L.first && (fp.diag & 1)) {  // test hook: no warm-up
+                s = L.off;
+                wr = 0;
+            }
+            walk_window(W, fp, tab, L, ch, L.act, s, wr, span, cnt, entry, exit, steps);
+        }
+        if (L.act) {
+            B.E[k0 + lane] = entry;
+            B.X[k0 + lane] = exit;
+            B.N[k0 + lane] = cnt;
+            B.F[k0 + lane] = L.first ? 1 : 0;
+        }
+        CDC_DIAG_T(5);
+    }
+    __syncthreads();
+
+    // 5-6. block settle (round 0), then the look-back; a block whose entry
+    // turns out stale settles again from the predecessor's final exit (round 1).
+#pragma unroll 1
+    for (int round = 0; round < 2; ++round) {
+        bool need;
+        if (round == 0) {
+            const uint32_t k = threadIdx.x;
+            need = __syncthreads_or(k > 0 && k < nsp && !B.F[k] && B.E[k] != B.X[k - 1]) != 0;
+        } else {
+            if (wave == 0) {
+                uint64_t C = 0;
+                for (uint32_t k = lane; k < nsp; k += 64) C += B.N[k];
+                C = wave_sum(C);
+                const uint64_t Eb = B.F[0] ? kNoDep : B.E[0];
+                const uint64_t Xb = B.X[nsp - 1];
+                uint64_t acc = 0, pred = 0;
+                int ok = 1;
+                if (b > 0) {
+                    publish(rs, b, kAgg, C, Eb, Xb, lane);
+                    ok = lookback(rs, b, Eb, lane, acc, pred);
+                }
+                if (ok != 0) publish(rs, b, kInc, acc + C, 0, Xb, lane);  // (a timeout too: never strand waiters)
+                if (lane == 0) {
+                    B.base = acc;
+                    B.pred = pred;
+                    B.rewalk = ok == 0 ? 1u : 0u;
+                    if (ok < 0) atomicAdd((unsigned long long *)&cp.stats[kStatError], 1ull);
+                }
+                CDC_DIAG_T(6);
+            }
+            __syncthreads();
+            need = B.rewalk != 0;
+        }
+        if (need) {
+            for (uint32_t w2 = 0; w2 < (uint32_t)kResWaves; ++w2) {
+                if (wave == w2 && k0 < nsp)
+                    wave_settle(st, fp, cand, tab, ch, W, dense, L, lane, k0, w2 > 0 || round > 0,
+                                w2 > 0 ? B.X[k0 - 1] : B.pred, B, span, rewalks, steps);
+                __syncthreads();
+            }
+        }
+    }
+    if (B.rewalk && wave == 0) {
+        uint64_t C = 0;
+        for (uint32_t k = lane; k < nsp; k += 64) C += B.N[k];
+        C = wave_sum(C);
+        publish(rs, b, kInc, B.base + C, 0, B.X[nsp - 1], lane);
+    }
+
+    // 7. output: this wave's spans' chunks at their final index
+    if (k0 < nsp) {
+        uint32_t wpre0 = 0;
+        for (uint32_t k = 0; k < k0; ++k) wpre0 += B.N[k];
+        const uint32_t myN = L.act ? B.N[k0 + lane] : 0;
+        uint32_t x = myN;
+#pragma unroll
+        for (int o = 1; o < kWalkSpans; o <<= 1) {
+            const uint32_t t = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += t;
+        }
+        if (lane < kWalkSpans) W.wpre[lane + 1] = x;
+        if (lane == 0) W.wpre[0] = 0;
+        const uint32_t wtot = (uint32_t)__shfl(x, kWalkSpans - 1);
+        const uint64_t obase = B.base + wpre0;
+        const bool bad = __ballot(L.act && myN > ch.smax) != 0 || obase + wtot > out_cap;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's chunk-start stores, before its loads
+        wave_sync_lds();
+        if (!bad) {
+            for (uint32_t i = lane; i < wtot; i += 64) {
+                int k = 0;
+                while (k + 1 < kWalkSpans && W.wpre[k + 1] <= i) ++k;
+                const uint32_t r = i - W.wpre[k];
+                const uint64_t *list = ch.starts + (G0 + k) * ch.smax;
+                const uint64_t s0 = ld_nt(list + r);
+                const uint64_t nx = r + 1 < B.N[k0 + k] ? ld_nt(list + r + 1) : B.X[k0 + k];
+                out[obase + i] = cdc_chunk_pod{s0, nx - s0};
+            }
+            if (L.act) {
+                if (L.first) cp.h_first[L.si] = obase + x - myN;
+                if (L.g + 1 == st.total_spans) cp.h_first[st.n] = obase + x;
+            }
+        }
+        const uint64_t cs = wave_sum(cstat), rw = wave_sum(rewalks), sp = wave_sum(steps);
+        if (lane == 0) {
+            B.stat[wave][0] = cs;
+            B.stat[wave][1] = rw;
+            B.stat[wave][2] = sp + (bad ? (1ull << 40) : 0);
+        }
+        CDC_DIAG_T(7);
+    } else if (lane == 0) {
+        B.stat[wave][0] = B.stat[wave][1] = B.stat[wave][2] = 0;
+    }
+    if ((fp.diag & 128) && lane == 0)
+        for (int k = 0; k < kStatDiagN; ++k) B.diag[wave][k] = dt[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t cs = 0, rw = 0, sp = 0;
+        for (int w = 0; w < kResWaves; ++w) {
+            cs += B.stat[w][0];
+            rw += B.stat[w][1];
+            sp += B.stat[w][2];
+        }
+        if (fp.diag & 128)
+            for (int k = 0; k < kStatDiagN; ++k) {
+                uint64_t d = 0;
+                for (int w = 0; w < kResWaves; ++w) d += B.diag[w][k];
+                atomicAdd((unsigned long long *)&cp.stats[kStatDiag0 + k], (unsigned long long)d);
+            }
+        const uint64_t err = sp >> 40;
+        sp &= (1ull << 40) - 1;
+        if (cs) atomicAdd((unsigned long long *)&cp.stats[kStatCand], (unsigned long long)cs);
+        if (rw) atomicAdd((unsigned long long *)&cp.stats[kStatRewalk], (unsigned long long)rw);
+        if (sp) atomicAdd((unsigned long long *)&cp.stats[kStatOnDemand], (unsigned long long)sp);
         if (err) atomicAdd((unsigned long long *)&cp.stats[kStatError], (unsigned long long)err);
         __threadfence();
         if (atomicAdd((unsigned long long *)&cp.stats[kStatTicket], 1ull) + 1 == gridDim.x) {
             __threadfence();
-            for (int i = 0; i < kStatTicket; ++i)
-                cp.h_stats[i] = __hip_atomic_load(&cp.stats[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int i = 0; i < kStatWords; ++i)
+                if (i != kStatDone) cp.h_stats[i] = ld_agent(&cp.stats[i]);
+            const uint64_t c = cp.h_stats[kStatCand];
+            cp.h_stats[kStatCand] = c >> 24;
+            cp.h_stats[kStatOvf] = c & 0xFFFFFF;
             __threadfence_system();
             cp.h_stats[kStatDone] = 1;
         }
     }
 }
+#undef CDC_DIAG_T
 
 }  // namespace
 
@@ -1011,39 +1417,26 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
         else
             scan_tail_kernel<false><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, d_tails);
     }
-    const uint64_t groups = (st.total_spans + kScanWaves - 1) / kScanWaves;
+    // 16 waves per CU (the 128-VGPR budget), GEAR lookups one dword ahead of
+    // the chain.  (Measured: 12 waves with two dwords of lookahead is slower.)
+    constexpr int W = 16, K = 1;
+    const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
     if (fp.cm_align)
-        scan_kernel<true><<<grid, kScanThreads, 0, s>>>(st, fp, d_gear, cand, cp);
+        scan_kernel<true, W, K><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else
-        scan_kernel<false><<<grid, kScanThreads, 0, s>>>(st, fp, d_gear, cand, cp);
+        scan_kernel<false, W, K><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     return hipGetLastError();
 }
 
-hipError_t launch_chain(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
-                        const Candidates &cand, const Chains &ch, const Compact &cp, hipStream_t s) {
-    if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (unsigned)((st.total_spans + kResWaves - 1) / kResWaves);
-    chain_kernel<<<grid, kResThreads, 0, s>>>(st, fp, d_gear, cand, ch, cp);
-    return hipGetLastError();
-}
+uint64_t resolve_blocks(uint64_t spans) { return (spans + kBlockSpans - 1) / kBlockSpans; }
 
-hipError_t launch_fix(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
-                      const Candidates &cand, const Chains &ch, const Compact &cp, hipStream_t s) {
+hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
+                          const Candidates &cand, const Chains &ch, const Compact &cp, const Resolve &rs,
+                          void *d_out, uint64_t out_cap, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    const uint64_t nblocks = (st.total_spans + 63) / 64;
-    const unsigned grid = (unsigned)((nblocks + kResWaves - 1) / kResWaves);
-    for (int p = 0; p < kPasses; ++p) fix_kernel<<<grid, kResThreads, 0, s>>>(st, fp, d_gear, cand, ch, cp, p);
-    serial_kernel<<<1, 64, 0, s>>>(st, fp, d_gear, cand, ch, cp);
-    return hipGetLastError();
-}
-
-hipError_t launch_compact(const StreamTable &st, const Chains &ch, const Compact &cp, void *d_out,
-                          uint64_t out_cap, hipStream_t s) {
-    if (!st.total_spans) return hipSuccess;
-    const unsigned grid = (unsigned)((st.total_spans + kCompThreads - 1) / kCompThreads);
-    count_kernel<<<grid, kCompThreads, 0, s>>>(st, ch, cp);
-    write_kernel<<<grid, kCompThreads, 0, s>>>(st, ch, cp, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap);
+    resolve_kernel<<<(unsigned)resolve_blocks(st.total_spans), kResThreads, 0, s>>>(
+        st, fp, d_gear, cand, ch, cp, rs, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap);
     return hipGetLastError();
 }
 

@@ -128,6 +128,7 @@ typedef struct cdc_timing {
     uint64_t candidates;     /* candidate positions emitted by the scan */
     uint64_t bytes;          /* input bytes of the batch */
     double hash_ms;          /* last cdc_sha256_chunks_device / cdc_chunk_and_hash kernel time */
+    uint64_t walk_fallback_steps; /* chain-walk steps without a precomputed record link */
 } cdc_timing_t;
 
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t);
