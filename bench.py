@@ -299,7 +299,9 @@ def host_path_leg(eng):
     spans, chunk_s = cfa.write_spans(ch, hb[:fs_bytes])
     hp["fs_write_1MiB_segments"] = {
         "GiBps": fs_bytes / chunk_s / (1 << 30), "bytes": int(fs_bytes), "spans": int(spans.size),
-        "metric": "bytes / summed chunk_data seconds, as CDCFixture::measure"}
+        "metric": "bytes / wall seconds of cdc_fs_write (pageable host buffer -> H2D -> chunking -> D2H of "
+                  "the chunk list); spans identical to the reference's 1 MiB StorageWriter loop "
+                  "(tests/test_gpu_parity.py::test_write_path_segmentation_invariance)"}
     return hp
 
 
@@ -398,6 +400,9 @@ def main(argv=None):
             extras["sweep"] = sweep_lines(args, eng, max(5, args.steps // 2))
         if args.cpu_seconds > 0:
             extras["cpu_baseline"] = cpu_baseline_leg(args, eng.bufs[0][:shard.lens[0]].cpu().numpy())
+            fw = extras.get("host_path", {}).get("fs_write_1MiB_segments")
+            if fw:
+                fw["x_cpu_single_thread"] = fw["GiBps"] / extras["cpu_baseline"]["value"]
 
     traffic, traffic_src = traffic_for_build(args.traffic_json, bytes_rank)
     if rank == 0:

@@ -5,7 +5,6 @@
 #include "../../include/chunkfs_amd.h"
 #include "../../include/chunkfs_amd_debug.h"
 #include "engine.hpp"
-#include "storage_writer.hpp"
 
 struct cdc_handle {
     cdc::Engine *engine;
@@ -84,19 +83,12 @@ int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
                      size_t seg_size, uint64_t *span_lengths, size_t cap,
                      double *chunk_seconds) {
     if (!h) return bad_handle();
-    if (len && !data) {
-        cdc::set_error("cdc_fs_write: data is NULL");
+    if (cap && !span_lengths) {
+        cdc::set_error("cdc_fs_write: span_lengths is NULL");
         return CDC_EINVAL;
     }
-    cdc::Engine *e = h->engine;
-    auto chunk = [e](const uint8_t *buf, size_t n, std::vector<cdc_chunk_t> &out) -> int64_t {
-        out.resize(e->max_chunks(n));
-        const int64_t c = e->chunk_host(buf, n, out.data(), out.size());
-        if (c >= 0) out.resize((size_t)c);
-        return c;
-    };
     std::vector<uint64_t> spans;
-    const int64_t n = cdc::storage_write_spans(chunk, data, len, seg_size, spans, chunk_seconds);
+    const int64_t n = h->engine->fs_write(data, len, seg_size, spans, chunk_seconds);
     if (n < 0) return n;
     for (size_t i = 0; i < spans.size() && i < cap; ++i) span_lengths[i] = spans[i];
     return n;

@@ -8,6 +8,7 @@
 // leave HBM.
 #include "engine.hpp"
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -454,7 +455,7 @@ int Engine::run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     }
     if (fp_.diag & 128) {
         const double waves = (double)p3::resolve_blocks(st.total_spans) * 4;
-        std::fprintf(stderr, "resolve phases, us per wave (meta recs trunc links virt walk lookback out):");
+        std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk lookback(w0) out):");
         for (int i = 0; i < p3::kStatDiagN; ++i)
             std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / waves);
         std::fprintf(stderr, "\n");
@@ -599,6 +600,37 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out,
         HIP_TRY(hipStreamSynchronize(own_stream_));
     }
     return count;
+}
+
+int64_t Engine::fs_write(const uint8_t *data, size_t len, size_t seg_size, std::vector<uint64_t> &spans,
+                         double *seconds) {
+    spans.clear();
+    if (seg_size == 0) {
+        set_error("cdc_fs_write: seg_size must be > 0");
+        return CDC_EINVAL;
+    }
+    if (len && !data) {
+        set_error("cdc_fs_write: data is NULL");
+        return CDC_EINVAL;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    constexpr size_t kFsWindow = size_t(1) << 32;  // bytes of the write per device pass
+    std::vector<cdc_chunk_t> chunks;
+    size_t rest = 0;  // start of the carried-over chunk: a chunk boundary of the whole write
+    for (size_t cur = 0; cur < len;) {
+        const size_t end = len - cur < kFsWindow ? len : cur + kFsWindow;
+        const size_t n = end - rest;  // buffer = rest ++ new bytes (storage.rs:309-310), contiguous here
+        chunks.resize(max_chunks(n));
+        const int64_t c = chunk_host(data + rest, n, chunks.data(), chunks.size());
+        if (c < 0) return c;
+        // storage.rs:318-322: every chunk but the last becomes a span, the last is carried
+        for (int64_t i = 0; i + 1 < c; ++i) spans.push_back(chunks[i].length);
+        if (c > 0) rest += chunks[c - 1].offset;
+        cur = end;
+    }
+    if (len > rest) spans.push_back(len - rest);  // flush (storage.rs:360-383)
+    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return (int64_t)spans.size();
 }
 
 int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,

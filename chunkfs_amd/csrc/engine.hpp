@@ -28,6 +28,15 @@ class Engine {
     // entries) also the SHA-256 of every chunk (StorageWriter's hashing).
     int64_t chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, size_t cap,
                        uint8_t *digests = nullptr);
+    // ChunkStorage::write of one whole write (storage.rs:78-103, 302-383):
+    // the span lengths the StorageWriter loop produces.  Both supported
+    // chunkers restart at every chunk boundary, so the carried-over `rest`
+    // always begins at a boundary of the whole write and the spans do not
+    // depend on the segment size: the write is chunked in
+    // device windows of up to kFsWindow bytes, each window's last chunk
+    // carried into the next exactly as the reference carries `rest`.
+    int64_t fs_write(const uint8_t *data, size_t len, size_t seg_size, std::vector<uint64_t> &spans,
+                     double *seconds);
     // SHA-256 of chunks of one device-resident stream (Sha256Hasher::hash).
     int sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
                       uint8_t *d_digests, hipStream_t s);

@@ -696,24 +696,22 @@ struct LaneSpan {
 // Walk every lane with go=true from s to its span's end, exact, from the
 // bytes and the global record lists (lane_next_global; across an overflowed
 // record list the whole wave steps with coop_next_bytes).  For windows too
-// dense for the LDS path.  Writes the starts >= off to the span's list.
+// dense for the LDS path.  The starts go through emit_start (below).
 // Wave-synchronous.
+struct ChainWin;
+__device__ __forceinline__ void emit_start(ChainWin &W, const Chains &ch, const LaneSpan &L, uint32_t l, uint64_t s,
+                                           uint32_t &cnt, uint64_t &entry);
 __device__ __forceinline__ void walk_lanes(const StreamTable &st, const FastParams &fp, const Candidates &cand,
-                                           const uint64_t *tab, const Chains &ch, const LaneSpan &L,
+                                           const uint64_t *tab, ChainWin &W, const Chains &ch, const LaneSpan &L,
                                            uint32_t lane, bool go, uint64_t s, uint32_t &cnt, uint64_t &entry,
                                            uint64_t &exit, uint64_t &steps) {
-    uint64_t *list = ch.starts + L.g * ch.smax;
     cnt = 0;
     entry = ~0ull;
     go = go && s < L.span_end;
     for (;;) {
         bool need = false;
         if (go) {
-            if (s >= L.off) {
-                if (cnt < ch.smax) list[cnt] = s;
-                if (cnt == 0) entry = s;
-                ++cnt;
-            }
+            emit_start(W, ch, L, lane, s, cnt, entry);
             ++steps;
             const uint64_t nx = lane_next_global(st, fp, cand, tab, L.data, L.n, L.gbase, s);
             if (nx == ~0ull) need = true; else s = nx;
@@ -766,13 +764,19 @@ constexpr uint64_t kNoDep = ~0ull;  // block entry of a block that starts a stre
 constexpr uint64_t kAgg = 1, kInc = 2;
 constexpr uint32_t kSpinMax = 1u << 26;  // look-back poll bound: an error, never a hang
 
+constexpr uint32_t kLdsStarts = 24;  // chunk starts per walked span kept in LDS (the rest: HBM)
+constexpr int kKeyShift = 40;        // record key: stream << 40 | stream offset (sorted in a window)
+constexpr uint64_t kKeyPos = (1ull << kKeyShift) - 1;
+
 struct ChainWin {
-    uint32_t rec[kWinRecs];           // the window's records, slot after slot
+    uint64_t key[kWinRecs];           // the window's records: stream << 40 | stream offset, sorted
+    uint32_t rec[kWinRecs];           // the records themselves (hit flags)
     uint32_t link[kWinRecs + kVirt];  // next start - entry position (0: not computed)
     uint16_t lrec[kWinRecs + kVirt];  // entry index + 1 of that next start (0: not an entry)
-    uint8_t tr[kWinRecs];             // truncated-region result of each record in reach
+    uint8_t rslot[kWinRecs];          // slot of each record
     uint8_t vslot[kVirt];             // virtual entries: slot, stream offset
     uint64_t vpos[kVirt];
+    uint32_t st[kWalkSpans][kLdsStarts];  // first chunk starts of each walked span (offset in span)
     uint64_t soff[kWinSlots];         // stream offset of each slot's span
     uint64_t slen[kWinSlots];         // its stream's length
     const uint8_t *sptr[kWinSlots];   // its stream's bytes
@@ -780,7 +784,7 @@ struct ChainWin {
     uint32_t scnt[kWinSlots];         // its records (> cap: overflowed)
     uint32_t pre[kWinSlots + 1];      // compact start of each slot's records
     uint32_t wpre[kWalkSpans + 1];    // output: chunk prefix of the walked spans
-    uint32_t nvirt;
+    uint32_t nrec, nvirt;
 };
 
 struct BlockState {
@@ -794,65 +798,51 @@ struct BlockState {
     uint64_t diag[kResWaves][kStatDiagN];  // per wave phase times (diag & 128)
 };
 
-// Slot of window record i.
-__device__ __forceinline__ int win_slot(const ChainWin &W, uint32_t i) {
-    int j = 0;
-    while (j + 1 < kWinSlots && W.pre[j + 1] <= i) ++j;
-    return j;
-}
+__device__ __forceinline__ uint64_t skey(uint32_t si) { return (uint64_t)si << kKeyShift; }
 
-// Local index of the first window record of stream si at or after p, or
-// kWinRecs when none.
-__device__ __forceinline__ uint32_t win_first_at(const ChainWin &W, uint32_t si, uint64_t p, uint64_t span) {
-#pragma unroll 1
-    for (int j = 0; j < kWinSlots; ++j) {
-        if (W.ssi[j] != si || W.soff[j] + span <= p) continue;
-        const uint32_t b0 = W.pre[j], b1 = W.pre[j + 1];
-        const uint32_t rel = p > W.soff[j] ? (uint32_t)(p - W.soff[j]) : 0u;
-        uint32_t a = b0, b = b1;
-        while (a < b) {
-            const uint32_t m = (a + b) >> 1;
-            if ((W.rec[m] & kCandPosMask) < rel) a = m + 1; else b = m;
-        }
-        if (a < b1) return a;
+// Index of the first window record whose key is >= k (nrec when none).
+__device__ __forceinline__ uint32_t win_lower(const ChainWin &W, uint64_t k) {
+    uint32_t a = 0, b = W.nrec;
+    while (a < b) {
+        const uint32_t m = (a + b) >> 1;
+        if (W.key[m] < k) a = m + 1; else b = m;
     }
-    return kWinRecs;
+    return a;
 }
 
-// Entry index + 1 of a start exactly at p (a record or a virtual entry), or 0.
-__device__ __forceinline__ uint32_t win_entry_at(const ChainWin &W, uint32_t si, uint64_t p, uint64_t span) {
-    const uint32_t f = win_first_at(W, si, p, span);
-    if (f < kWinRecs && W.soff[win_slot(W, f)] + (W.rec[f] & kCandPosMask) == p) return f + 1;
+// Entry index + 1 of a start exactly at p of stream si (a record or a
+// virtual entry), or 0.
+__device__ __forceinline__ uint32_t win_entry_at(const ChainWin &W, uint32_t si, uint64_t p) {
+    const uint64_t k = skey(si) | p;
+    const uint32_t f = win_lower(W, k);
+    if (f < W.nrec && W.key[f] == k) return f + 1;
     for (uint32_t v = 0; v < W.nvirt; ++v)
         if (W.vpos[v] == p && W.ssi[W.vslot[v]] == si) return kWinRecs + v + 1;
     return 0;
 }
 
 // First qualifying window record for a chunk starting at c (stream si,
-// regime R): a linear scan from local index i0 (records are position-sorted
-// within a stream across consecutive slots).  Returns the position, or
-// c + rem when none is below c + re.  *lr = local index + 1.
+// regime R): a linear scan from local index i0 over the sorted keys.
+// Returns the position, or c + rem when none is below c + re.  *lr = local
+// index + 1.
 __device__ __forceinline__ uint64_t win_search(const ChainWin &W, uint32_t si, uint64_t c, const Regime &R,
                                                uint32_t i0, uint32_t *lr) {
     *lr = 0;
-    const uint64_t lo = c + R.tl, hi = c + R.re;
-    int j = 0;
-    for (uint32_t i = i0;; ++i) {
-        while (j < kWinSlots && i >= W.pre[j + 1]) ++j;
-        if (j >= kWinSlots || W.ssi[j] != si) break;
-        const uint32_t r = W.rec[i];
-        const uint64_t p = W.soff[j] + (r & kCandPosMask);
-        if (p >= hi) break;
-        if (p >= lo && (r & ((p - c) < R.ce ? kCandHitS : kCandHitL))) {
+    const uint64_t s = skey(si);
+    const uint64_t lo = s | (c + R.tl), hi = s | (c + R.re), ce = s | (c + R.ce);
+    for (uint32_t i = i0; i < W.nrec; ++i) {
+        const uint64_t k = W.key[i];
+        if (k >= hi) break;
+        if (k >= lo && (W.rec[i] & (k < ce ? kCandHitS : kCandHitL))) {
             *lr = i + 1;
-            return p;
+            return k & kKeyPos;
         }
     }
     return c + R.rem;
 }
 
 // Next start after a chunk starting at c (stream si, n bytes): the truncated
-// result `tr` (or from the bytes when tr_known is false), else the first
+// result `tr` (or from the bytes when kTrKnown is false), else the first
 // qualifying window record from local index i0 on, else the max / end cut.
 // *lr = local index + 1 of the result when it is a window record.
 template <bool kTrKnown>
@@ -867,6 +857,7 @@ __device__ __forceinline__ uint64_t win_next(const ChainWin &W, const FastParams
         if (t != kTruncNone) return c + R.a0 + t;
     }
     if (R.tl >= R.re) return c + R.rem;
+    if (fp.diag & 8) return c + R.rem;  // timing experiment only
     return win_search(W, si, c, R, i0, lr);
 }
 
@@ -880,53 +871,32 @@ __device__ __forceinline__ uint32_t virt_alloc(bool mk, uint32_t &nv) {
     return v < kVirt ? v : kVirt;
 }
 
-// Link of the chunk starting at c (window slot j) into W.link/W.lrec[e]; a
-// next start that is not a record but lies in a walked slot becomes a new
-// virtual entry.  Wave-synchronous (all lanes call; act = has an entry).
-template <bool kTrKnown>
-__device__ __forceinline__ void link_entry(ChainWin &W, const FastParams &fp, const uint64_t *tab, bool act,
-                                           uint32_t e, int j, uint64_t c, uint32_t i0, uint32_t tr, uint32_t sl2,
-                                           uint32_t &nv) {
-    bool mk = false;
-    uint64_t nx = 0;
-    uint32_t lr = 0;
-    int jt = 0;
-    if (act) {
-        const uint32_t si = W.ssi[j];
-        const uint64_t n = W.slen[j];
-        nx = win_next<kTrKnown>(W, fp, tab, W.sptr[j], n, si, c, i0, tr, &lr);
-        W.link[e] = (uint32_t)(nx - c);
-        jt = j + (int)((nx - W.soff[j]) >> sl2);  // <= j + 1: max <= span
-        mk = lr == 0 && nx < n && jt < kReach && W.ssi[jt] == si;
+// Record the start s of the walked span in lane slot l: the first
+// kLdsStarts in LDS, the rest in HBM.
+__device__ __forceinline__ void emit_start(ChainWin &W, const Chains &ch, const LaneSpan &L, uint32_t l, uint64_t s,
+                                           uint32_t &cnt, uint64_t &entry) {
+    if (s >= L.off) {
+        if (cnt < kLdsStarts) W.st[l][cnt] = (uint32_t)(s - L.off);
+        else if (cnt < ch.smax) ch.starts[L.g * ch.smax + cnt] = s;
+        if (cnt == 0) entry = s;
+        ++cnt;
     }
-    const uint32_t v = virt_alloc(mk, nv);
-    if (mk && v < kVirt) {
-        W.vpos[v] = nx;
-        W.vslot[v] = (uint8_t)jt;
-        lr = kWinRecs + v + 1;
-    }
-    if (act) W.lrec[e] = (uint16_t)lr;
 }
 
 // Walk every lane with go=true from s (entry index + 1 wr, 0: none) to its
-// span's end over the window links, writing the starts >= off to the span's
-// list.  A start without a link (a stream start, a spent virtual budget) takes
-// one exact step from the bytes.  Wave-synchronous.
-__device__ __forceinline__ void walk_window(const ChainWin &W, const FastParams &fp, const uint64_t *tab,
-                                            const LaneSpan &L, const Chains &ch, bool go, uint64_t s, uint32_t wr,
-                                            uint64_t span, uint32_t &cnt, uint64_t &entry, uint64_t &exit,
+// span's end over the window links.  A start without a link (a stream start,
+// a spent virtual budget) takes one exact step from the bytes.
+// Wave-synchronous.
+__device__ __forceinline__ void walk_window(ChainWin &W, const FastParams &fp, const uint64_t *tab,
+                                            const LaneSpan &L, const Chains &ch, uint32_t lane, bool go, uint64_t s,
+                                            uint32_t wr, uint32_t &cnt, uint64_t &entry, uint64_t &exit,
                                             uint64_t &steps) {
-    uint64_t *list = ch.starts + L.g * ch.smax;
     cnt = 0;
     entry = ~0ull;
     go = go && s < L.span_end;
     for (;;) {
         while (go) {
-            if (s >= L.off) {
-                if (cnt < ch.smax) list[cnt] = s;
-                if (cnt == 0) entry = s;
-                ++cnt;
-            }
+            emit_start(W, ch, L, lane, s, cnt, entry);
             if (wr == 0) break;
             const uint32_t d = W.link[wr - 1];
             if (d == 0) break;
@@ -938,7 +908,7 @@ __device__ __forceinline__ void walk_window(const ChainWin &W, const FastParams 
         if (go) {
             ++steps;
             uint32_t lr;
-            s = win_next<false>(W, fp, tab, L.data, L.n, L.si, s, win_first_at(W, L.si, s, span), 0, &lr);
+            s = win_next<false>(W, fp, tab, L.data, L.n, L.si, s, win_lower(W, skey(L.si) | s), 0, &lr);
             wr = lr;
             go = s < L.span_end;
         }
@@ -951,10 +921,9 @@ __device__ __forceinline__ void walk_window(const ChainWin &W, const FastParams 
 // predecessor's exit (lane 0's predecessor: pred0, when has0).  Lanes
 // 0..kWalkSpans-1 own the wave's spans B.*[k0 + lane].
 __device__ __forceinline__ void wave_settle(const StreamTable &st, const FastParams &fp, const Candidates &cand,
-                                            const uint64_t *tab, const Chains &ch, const ChainWin &W, bool dense,
+                                            const uint64_t *tab, const Chains &ch, ChainWin &W, bool dense,
                                             const LaneSpan &L, uint32_t lane, uint32_t k0, bool has0,
-                                            uint64_t pred0, BlockState &B, uint64_t span, uint64_t &rewalks,
-                                            uint64_t &steps) {
+                                            uint64_t pred0, BlockState &B, uint64_t &rewalks, uint64_t &steps) {
     const bool mine = lane < kWalkSpans && L.act;
     uint64_t E = mine ? B.E[k0 + lane] : 0, X = mine ? B.X[k0 + lane] : 0;
     for (;;) {
@@ -967,10 +936,10 @@ __device__ __forceinline__ void wave_settle(const StreamTable &st, const FastPar
         uint32_t cnt = 0;
         uint64_t entry = 0, exit = 0;
         if (dense)
-            walk_lanes(st, fp, cand, tab, ch, L, lane, ready, pred, cnt, entry, exit, steps);
+            walk_lanes(st, fp, cand, tab, W, ch, L, lane, ready, pred, cnt, entry, exit, steps);
         else
-            walk_window(W, fp, tab, L, ch, ready, pred, ready ? win_entry_at(W, L.si, pred, span) : 0u, span, cnt,
-                        entry, exit, steps);
+            walk_window(W, fp, tab, L, ch, lane, ready, pred, ready ? win_entry_at(W, L.si, pred) : 0u, cnt, entry,
+                        exit, steps);
         if (ready) {
             B.E[k0 + lane] = E = entry;
             B.X[k0 + lane] = X = exit;
@@ -978,6 +947,102 @@ __device__ __forceinline__ void wave_settle(const StreamTable &st, const FastPar
             ++rewalks;
         }
     }
+}
+
+// One entry of the link pass: a record in reach or a virtual entry, with the
+// parameters of its truncated region (fast: its 52 bytes lie before n).
+struct LinkItem {
+    bool act, fast;
+    int j;
+    uint32_t e, i0, si, len;
+    uint64_t c, n, a0, ce, w0;
+    const uint8_t *data;
+};
+
+__device__ __forceinline__ LinkItem link_item(const ChainWin &W, const FastParams &fp, bool virt, uint32_t x,
+                                              uint32_t e1) {
+    LinkItem it{};
+    it.act = x < e1;
+    if (!it.act) return it;
+    if (virt) {
+        it.e = kWinRecs + x;
+        it.j = W.vslot[x];
+        it.c = W.vpos[x];
+        it.i0 = win_lower(W, skey(W.ssi[it.j]) | it.c);
+    } else {
+        it.e = x;
+        it.j = W.rslot[x];
+        it.c = W.key[x] & kKeyPos;
+        it.i0 = x + 1;
+    }
+    it.si = W.ssi[it.j];
+    it.n = W.slen[it.j];
+    it.data = W.sptr[it.j];
+    if (it.n - it.c > fp.min) {
+        const Regime R = regime(fp, it.c, it.n);
+        if (R.tl > R.a0) {
+            it.len = (uint32_t)(R.tl - R.a0);
+            it.a0 = R.a0;
+            it.ce = R.ce;
+            it.w0 = it.c + R.a0;
+            it.fast = (it.w0 & ~3ull) + 52 <= it.n;
+        }
+    }
+    return it;
+}
+
+// The 13 dwords holding an item's truncated region (a harmless read of
+// `safe` when it has none in reach).  (Four 16-byte loads plus a select
+// realignment measured slower: the extra registers cost occupancy.)
+__device__ __forceinline__ void item_load(const LinkItem &it, const void *safe, uint32_t (&w)[13]) {
+    const uint8_t *src = it.fast ? it.data + (it.w0 & ~3ull) : static_cast<const uint8_t *>(safe);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(src + 4 * i);
+}
+
+__device__ __forceinline__ uint32_t item_trunc(const LinkItem &it, const uint32_t (&w)[13], const FastParams &fp,
+                                               const uint64_t *tab) {
+    if (!it.act || it.len == 0) return kTruncNone;
+    if (!it.fast) return trunc_call(it.data, it.n, it.c, fp, tab);
+    const uint32_t r = (uint32_t)(it.w0 & 3);
+    uint64_t h = 0;
+    uint32_t t = kTruncNone;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const uint32_t a = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t d = 4 * k + b;
+            if (d >= kTruncMax) break;
+            h = shl1_add(h, tab[(a >> (8 * b)) & 255]);
+            const bool hit = d < it.len && !(h & ((it.a0 + d) < it.ce ? fp.mask_s : fp.mask_l));
+            t = (hit && t == kTruncNone) ? d : t;
+        }
+    }
+    return t;
+}
+
+// The item's link into W.link/W.lrec; a next start that is neither a record
+// nor past the walked slots becomes a new virtual entry.  Wave-synchronous.
+__device__ __forceinline__ void item_link(ChainWin &W, const FastParams &fp, const uint64_t *tab,
+                                          const LinkItem &it, uint32_t tr, uint32_t sl2, uint32_t &nv) {
+    bool mk = false;
+    uint64_t nx = 0;
+    uint32_t lr = 0;
+    int jt = 0;
+    if (it.act) {
+        nx = win_next<true>(W, fp, tab, nullptr, it.n, it.si, it.c, it.i0, tr, &lr);
+        W.link[it.e] = (uint32_t)(nx - it.c);
+        jt = it.j + (int)((nx - W.soff[it.j]) >> sl2);  // <= j + 1: max <= span
+        mk = lr == 0 && nx < it.n && jt < kReach && W.ssi[jt] == it.si;
+    }
+    const uint32_t v = virt_alloc(mk, nv);
+    if (mk && v < kVirt) {
+        W.vpos[v] = nx;
+        W.vslot[v] = (uint8_t)jt;
+        lr = kWinRecs + v + 1;
+    }
+    if (it.act) W.lrec[it.e] = (uint16_t)lr;
 }
 
 // Inter-block words (MI355X_MICROARCH.md "inter-workgroup visibility"; the
@@ -1100,7 +1165,7 @@ __device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) {
 // timing experiments only, 0 in every real run: 1 = walks start at the span
 // start (no warm-up: nearly every boundary re-walks), 2 = every wave takes the
 // dense (global record list) path, 128 = phase timings into the stats.
-__global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable st, const FastParams fp,
+__global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTable st, const FastParams fp,
                                                               const uint64_t *__restrict__ gear,
                                                               const Candidates cand, const Chains ch,
                                                               const Compact cp, const Resolve rs,
@@ -1164,6 +1229,7 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
             }
             if (acc > kWinRecs) dn = true;
             W.pre[kWinSlots] = dn ? 0 : acc;
+            W.nrec = dn ? 0 : acc;
             W.nvirt = dn ? 1u : 0u;  // (the dense flag, for the other lanes)
         }
         wave_sync_lds();
@@ -1190,9 +1256,9 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
             uint64_t s0 = 0;
             if (L.act && !L.first) s0 = L.off > kWarmSpans * span ? L.off - kWarmSpans * span : 0;
             if (L.act && !L.first && (fp.diag & 1)) s0 = L.off;  // test hook: no warm-up
-            walk_lanes(st, fp, cand, tab, ch, L, lane, L.act, s0, cnt, entry, exit, steps);
+            walk_lanes(st, fp, cand, tab, W, ch, L, lane, L.act, s0, cnt, entry, exit, steps);
         } else {
-            const uint32_t nrec = W.pre[kWinSlots];
+            const uint32_t nrec = W.nrec;
             {
                 uint32_t v[kWinSlots];
 #pragma unroll
@@ -1200,53 +1266,50 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
                     const uint32_t c = W.scnt[j];
                     v[j] = cand.pos[lane < c ? (uint64_t)(gfirst + j) * cap + lane : 0];
                 }
-#pragma unroll
-                for (int j = 0; j < kWinSlots; ++j)
-                    if (lane < W.scnt[j]) W.rec[W.pre[j] + lane] = v[j];
 #pragma unroll 1
-                for (int j = 0; j < kWinSlots; ++j)  // slots with more than 64 records
-                    for (uint32_t k = lane + 64; k < W.scnt[j]; k += 64)
-                        W.rec[W.pre[j] + k] = cand.pos[(uint64_t)(gfirst + j) * cap + k];
+                for (int j = 0; j < kWinSlots; ++j) {
+                    const uint64_t kb = skey(W.ssi[j]) | W.soff[j];
+                    const uint32_t c = W.scnt[j], p0 = W.pre[j];
+                    for (uint32_t k = lane; k < c; k += 64) {  // (k >= 64: rare dense-ish slots)
+                        const uint32_t r = k < 64 ? v[0] : cand.pos[(uint64_t)(gfirst + j) * cap + k];
+                        W.rec[p0 + k] = r;
+                        W.key[p0 + k] = kb + (r & kCandPosMask);
+                        W.rslot[p0 + k] = (uint8_t)j;
+                    }
+#pragma unroll
+                    for (int q = 0; q + 1 < kWinSlots; ++q) v[q] = v[q + 1];  // next slot's batch into v[0]
+                }
             }
             wave_sync_lds();
             CDC_DIAG_T(1);
-            // 2. truncated-region results of the records in reach
+            // 2-3. per entry (records in reach, then virtual entries until none
+            // is new): its truncated-region result, then its link -- the next
+            // chunk start after a chunk starting there -- by an LDS search.
+            // Next starts that are neither records nor past the walked slots
+            // become new virtual entries.
             const uint32_t nlink = W.pre[kReach];
-            for (uint32_t i = lane; i < nlink; i += 64) {
-                const int j = win_slot(W, i);
-                W.tr[i] = (uint8_t)trunc_bytes(W.sptr[j], W.slen[j], W.soff[j] + (W.rec[i] & kCandPosMask), fp, tab);
-            }
             for (uint32_t i = nlink + lane; i < nrec; i += 64) W.link[i] = 0;  // searched only
-            wave_sync_lds();
-            CDC_DIAG_T(2);
-            // 3. links: records in reach, then virtual entries until none is new
-            uint32_t nv = 0;
-            for (uint32_t base = 0; base < nlink; base += 64) {
-                const uint32_t i = base + lane;
-                const bool act = i < nlink;
-                const int j = act ? win_slot(W, i) : 0;
-                const uint64_t c = act ? W.soff[j] + (W.rec[i] & kCandPosMask) : 0;
-                link_entry<true>(W, fp, tab, act, i, j, c, i + 1, act ? W.tr[i] : 0u, sl2, nv);
-            }
-            wave_sync_lds();
-            CDC_DIAG_T(3);
-            for (uint32_t v0 = 0;;) {
-                const uint32_t v1 = min(nv, kVirt);
-                if (v0 >= v1) break;
-                for (uint32_t base = v0; base < v1; base += 64) {
-                    const uint32_t v = base + lane;
-                    const bool act = v < v1;
-                    const int j = act ? (int)W.vslot[v] : 0;
-                    const uint64_t c = act ? W.vpos[v] : 0;
-                    const uint32_t i0 = act ? win_first_at(W, W.ssi[j], c, span) : 0u;
-                    link_entry<false>(W, fp, tab, act, kWinRecs + v, j, c, i0, 0, sl2, nv);
+            uint32_t nv = 0, e0 = 0, e1 = nlink;
+            bool virt = false;
+            for (;;) {
+                for (uint32_t base = e0; base < e1; base += 64) {
+                    const LinkItem A = link_item(W, fp, virt, base + lane, e1);
+                    uint32_t wa[13];
+                    item_load(A, gear, wa);
+                    const uint32_t tr = (fp.diag & 4) ? kTruncNone : item_trunc(A, wa, fp, tab);
+                    item_link(W, fp, tab, A, tr, sl2, nv);
                 }
                 wave_sync_lds();
-                v0 = v1;
+                if (!virt) CDC_DIAG_T(4);
+                const uint32_t vend = min(nv, kVirt);
+                if (virt ? e1 >= vend : vend == 0) break;
+                e0 = virt ? e1 : 0;
+                e1 = vend;
+                virt = true;
             }
             if (lane == 0) W.nvirt = min(nv, kVirt);
             wave_sync_lds();
-            CDC_DIAG_T(4);
+            CDC_DIAG_T(3);
             // 4. the walks, from the first record kWarmSpans spans back (exact
             // from a stream start)
             uint64_t s = 0;
@@ -1255,7 +1318,7 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
                 const int jw = (int)lane;  // slot of span g - kWarmSpans
                 if (W.pre[jw + 1] > W.pre[jw]) {
                     wr = W.pre[jw] + 1;
-                    s = W.soff[jw] + (W.rec[W.pre[jw]] & kCandPosMask);
+                    s = W.key[W.pre[jw]] & kKeyPos;
                 } else {
                     s = W.soff[jw];
                 }
@@ -1264,7 +1327,7 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
                 s = L.off;
                 wr = 0;
             }
-            walk_window(W, fp, tab, L, ch, L.act, s, wr, span, cnt, entry, exit, steps);
+            walk_window(W, fp, tab, L, ch, lane, L.act, s, wr, cnt, entry, exit, steps);
         }
         if (L.act) {
             B.E[k0 + lane] = entry;
@@ -1313,11 +1376,12 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
             for (uint32_t w2 = 0; w2 < (uint32_t)kResWaves; ++w2) {
                 if (wave == w2 && k0 < nsp)
                     wave_settle(st, fp, cand, tab, ch, W, dense, L, lane, k0, w2 > 0 || round > 0,
-                                w2 > 0 ? B.X[k0 - 1] : B.pred, B, span, rewalks, steps);
+                                w2 > 0 ? B.X[k0 - 1] : B.pred, B, rewalks, steps);
                 __syncthreads();
             }
         }
     }
+    CDC_DIAG_T(2);
     if (B.rewalk && wave == 0) {
         uint64_t C = 0;
         for (uint32_t k = lane; k < nsp; k += 64) C += B.N[k];
@@ -1349,8 +1413,10 @@ __global__ __launch_bounds__(kResThreads) void resolve_kernel(const StreamTable 
                 while (k + 1 < kWalkSpans && W.wpre[k + 1] <= i) ++k;
                 const uint32_t r = i - W.wpre[k];
                 const uint64_t *list = ch.starts + (G0 + k) * ch.smax;
-                const uint64_t s0 = ld_nt(list + r);
-                const uint64_t nx = r + 1 < B.N[k0 + k] ? ld_nt(list + r + 1) : B.X[k0 + k];
+                const uint64_t off_k = W.soff[kWarmSpans + k];
+                const uint64_t s0 = r < kLdsStarts ? off_k + W.st[k][r] : ld_nt(list + r);
+                const uint64_t nx = r + 1 >= B.N[k0 + k] ? B.X[k0 + k]
+                                    : r + 1 < kLdsStarts ? off_k + W.st[k][r + 1] : ld_nt(list + r + 1);
                 out[obase + i] = cdc_chunk_pod{s0, nx - s0};
             }
             if (L.act) {

@@ -135,11 +135,15 @@ int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t);
 
 /* ---- Write path mirror --------------------------------
  * ChunkStorage::write (storage.rs:78-103) + StorageWriter::{write,flush}
- * (storage.rs:302-383) for ONE write call: 1 MiB (seg_size) slices, carry-over
+ * (storage.rs:302-383) for ONE write call: seg_size (1 MiB) slices, carry-over
  * of the last chunk of every segment, flush of the rest.  Writes the span
  * lengths in file order (min(count, cap) of them) and returns the span count.
- * *chunk_seconds (may be NULL) receives the summed wall time of the
- * chunk_data calls only, as the reference times it (storage.rs:314-316). */
+ * FastCDC and fixed-size chunking restart at every chunk boundary, so the
+ * spans do not depend on seg_size (> 0): the library uploads the write once
+ * and chunks it in device windows of up to 4 GiB with the same carry-over.
+ * *chunk_seconds (may be NULL) receives the wall time of the whole call
+ * (H2D + chunking + D2H), the device path's counterpart of the reference's
+ * summed chunk_data time (storage.rs:314-316). */
 int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
                      size_t seg_size, uint64_t *span_lengths, size_t cap,
                      double *chunk_seconds);

@@ -184,7 +184,9 @@ int64_t oracle_fs_write(int algo, const uint8_t *data, uint64_t len,
             *chunk_seconds += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
         if (n < 0) { free(buf); free(tmp_len); return -1; }
         cur += take;
-        if (n == 0) { rest = blen; continue; } /* storage.rs:318-320 (unreachable for non-empty) */
+        /* storage.rs:318-320: no chunks -> early return, rest unchanged (the
+         * slice is dropped; unreachable for non-empty buffers) */
+        if (n == 0) continue;
         uint64_t consumed = 0;
         for (int64_t i = 0; i < n - 1; i++) {
             if (nspans < cap && span_lengths) span_lengths[nspans] = tmp_len[i];
