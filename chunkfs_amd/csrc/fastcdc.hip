@@ -85,9 +85,7 @@ __device__ __forceinline__ uint32_t cand_test(uint64_t h, const FastParams &fp) 
 // h = (h << 1) + g as ONE opaque v_lshl_add_u64: plain C lets LLVM
 // reassociate the 48-term chain into a tree that keeps every lookup live.
 __device__ __forceinline__ uint64_t shl1_add(uint64_t h, uint64_t g) {
-    uint64_t r;
-    asm("v_lshl_add_u64 %0, %1, 1, %2" : "=v"(r) : "v"(h), "v"(g));
-    return r;
+    return (h << 1) + g;
 }
 
 // DPP wave_shr:1 (dpp_ctrl 0x138): lane i receives lane i-1; lane 0 keeps `fill`.
@@ -387,7 +385,7 @@ struct ScanLds {
 // hashes it serially from hash 0; its first 48 positions are re-tested at the
 // end with the true carry-in (lane l-1's final hash, one DPP shift; lane 0's
 // from the 48 bytes before the span).  Ragged last spans: scan_tail_kernel.
-template <bool kAlign, int kW, int kLook>
+template <bool kAlign, int kW, int kLook, int kMode>
 __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, const FastParams fp,
                                                            const uint64_t *__restrict__ gear,
                                                            const Candidates cand, const Compact cp) {
@@ -452,17 +450,24 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         F2 = C.q[2];
         gload_step(A, gp, istride, 2);
         SCHED_FENCE();
+// kMode: 0 = the scan; 1 = loads and transposes only, 2 = hashing only (timing
+// experiments: CHUNKFS_AMD_DIAG bits 8-9, results meaningless).
+#define CDC_PROC(POS, SKIP)                                                                    \
+    do {                                                                                       \
+        if constexpr (kMode == 1) h ^= (uint64_t)(C.q[0].x ^ C.q[1].y ^ C.q[2].z ^ C.q[3].w);   \
+        else process_step<kAlign, kLook>(C, h, POS, SKIP, ne, E, tab, rep, fp);                \
+    } while (0)
 #define CDC_SCAN_PAIR(T, LOAD_B, STAGE_A, LOAD_A)                                              \
     do {                                                                                       \
-        process_step<kAlign, kLook>(C, h, lo + (T) * kStep, (T) == 0 ? 3u : 0u, ne, E, tab, rep, fp); \
+        CDC_PROC(lo + (T) * kStep, (T) == 0 ? 3u : 0u);                                        \
         SCHED_FENCE();                                                                         \
         stage_step(C, B, wrow, rrow);                                                          \
-        if (LOAD_B) gload_step(B, gp, istride, (T) + 3);                                       \
+        if (LOAD_B && kMode != 2) gload_step(B, gp, istride, (T) + 3);                         \
         SCHED_FENCE();                                                                         \
-        process_step<kAlign, kLook>(C, h, lo + ((T) + 1) * kStep, 0u, ne, E, tab, rep, fp);    \
+        CDC_PROC(lo + ((T) + 1) * kStep, 0u);                                                  \
         SCHED_FENCE();                                                                         \
         if (STAGE_A) stage_step(C, A, wrow, rrow);                                             \
-        if (LOAD_A) gload_step(A, gp, istride, (T) + 4);                                       \
+        if (LOAD_A && kMode != 2) gload_step(A, gp, istride, (T) + 4);                         \
         SCHED_FENCE();                                                                         \
     } while (0)
         uint32_t t = 0;
@@ -470,6 +475,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         CDC_SCAN_PAIR(t, true, true, false);        // steps-4, steps-3
         CDC_SCAN_PAIR(t + 2, false, false, false);  // steps-2, steps-1
 #undef CDC_SCAN_PAIR
+#undef CDC_PROC
         // This span's carry-in bytes and identity, then the next span's prefetch.
         const uint64_t g_cur = g, off_cur = off;
         const uint32_t wb_cur = wb;
@@ -1488,10 +1494,15 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
     constexpr int W = 16, K = 1;
     const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
-    if (fp.cm_align)
-        scan_kernel<true, W, K><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+    const uint32_t mode = (fp.diag >> 8) & 3;
+    if (mode == 1 && fp.cm_align)
+        scan_kernel<true, W, K, 1><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+    else if (mode == 2 && fp.cm_align)
+        scan_kernel<true, W, K, 2><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+    else if (fp.cm_align)
+        scan_kernel<true, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else
-        scan_kernel<false, W, K><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+        scan_kernel<false, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     return hipGetLastError();
 }
 
