@@ -11,8 +11,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libchunkfs_amd.so")
-SOURCES = ["fastcdc.hip", "cdc_kernels.hip", "pipeline_v1.hip", "sha256.hip", "index.hip", "engine.cpp", "capi.cpp", "index_host.cpp"]
-HEADERS = ["fastcdc.hpp", "cdc_kernels.hpp", "pipeline_v1.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
+SOURCES = ["fastcdc.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "capi.cpp", "index_host.cpp"]
+HEADERS = ["fastcdc.hpp", "cdc_kernels.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]

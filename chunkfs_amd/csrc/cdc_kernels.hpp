@@ -1,17 +1,14 @@
-// cdc_kernels.hpp -- launch interface of the gfx950 chunking kernels.
+// cdc_kernels.hpp -- types shared by the gfx950 chunking kernels, and the
+// fixed-size / input-generator launchers (util_kernels.hip).  The FastCDC
+// pipeline's launchers are in fastcdc.hpp.
 //
-// Data layout in HBM (DESIGN.md "Layout"):
-//   * streams: caller-owned device buffers, 16-byte aligned, read exactly once
-//     by the scan kernel (the only HBM-bound kernel).
+// Data layout in HBM (DESIGN.md "Data layout"):
+//   * streams: caller-owned device buffers, 16-byte aligned, read once by the
+//     scan (the only HBM-bound kernel).
 //   * spans: every stream is cut into SPAN = 2^span_log2 byte spans; span g of
 //     the batch belongs to stream i with span_base[i] <= g < span_base[i+1].
-//     A span is both the scan unit and the resolve unit (one wavefront each).
 //   * candidates: per span, count[g] and up to `cap` u32 records
-//     pos[g*cap+k] (offset in span | truncated result | exact hit flags), in
-//     increasing position order.
-//   * chains: per span the speculative list of chunk starts and, when the
-//     look-back finds it stale, the re-walked one (starts[b][g*smax+k], u64
-//     stream offsets); per-span look-back descriptors (Lookback).
+//     pos[g*cap+k] (offset in span | exact hit flags), in position order.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -49,7 +46,7 @@ struct FastParams {
     uint32_t cm32;           // aligned: (cmask << tshift) >> 32
     uint32_t cm_lo, cm_hi;   // general form
     uint64_t mask_s_sh, mask_l_sh;  // mask_s / mask_l << tshift (exact flush tests)
-    uint32_t diag;           // timing experiments only (CHUNKFS_AMD_DIAG); 0 in every real run
+    uint32_t diag;           // test hooks / timing experiments (CHUNKFS_AMD_DIAG); 0 in every real run
 };
 
 struct Candidates {
@@ -58,36 +55,8 @@ struct Candidates {
     uint32_t *pos;    // [spans*cap]: offset in span (bits 0-23) | bit30 mask_l hit | bit31 mask_s hit
 };
 
-struct Chains {
-    uint32_t smax;
-    uint64_t *starts[2];   // [spans*smax]: chunk starts of each span (starts[1] unused)
-};
-
-// Single-pass resolve state (decoupled look-back over spans, in ticket
-// order).  Reset by the scan kernel of the same batch.
-struct Lookback {
-    uint64_t *desc;     // [waves of 64 spans]: status(62-63) | chunk count (25-61) | exit - span end (0-24)
-    uint64_t *ent;      // [waves]: valid(63) | starts a stream(62) | lane 0's entry - its span start
-    uint32_t *ticket;   // [2]: next span-group ticket, finished groups
-    uint64_t *stats;    // [4] device accumulators: candidates, overflowed spans, re-walked spans, timeouts
-    uint64_t *h_stats;  // host-mapped [4]: copy of stats, written by the last group
-    uint64_t *h_first;  // host-mapped [n+1]: index of each stream's first chunk
-};
-
-hipError_t launch_scan(const StreamTable &st, const FastParams &fp,
-                       const uint64_t *d_gear, const Candidates &cand,
-                       const Lookback &lb, int num_cus, hipStream_t s);
-hipError_t launch_next(const StreamTable &st, const FastParams &fp,
-                       const uint64_t *d_gear, const Candidates &cand, uint64_t *nxt,
-                       hipStream_t s);
-hipError_t launch_resolve(const StreamTable &st, const FastParams &fp,
-                          const uint64_t *d_gear, const Candidates &cand,
-                          const uint64_t *nxt, const Chains &ch, const Lookback &lb,
-                          void *d_out, uint64_t out_cap, hipStream_t s);
-hipError_t launch_fixed(const StreamTable &st, uint64_t chunk_size,
-                        const uint64_t *d_first, void *d_out, uint64_t total,
-                        hipStream_t s);
-hipError_t launch_fill_splitmix64(uint8_t *d_buf, uint64_t len, uint64_t seed,
-                                  hipStream_t s);
+hipError_t launch_fixed(const StreamTable &st, uint64_t chunk_size, const uint64_t *d_first, void *d_out,
+                        uint64_t total, hipStream_t s);
+hipError_t launch_fill_splitmix64(uint8_t *d_buf, uint64_t len, uint64_t seed, hipStream_t s);
 
 }  // namespace cdc

@@ -69,10 +69,6 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
     e->avg_ = avg;
     e->max_ = max;
     e->device_ = device;
-    if (const char *pv = std::getenv("CHUNKFS_AMD_PIPELINE")) {
-        const int v = std::atoi(pv);
-        e->pipeline_ = (v == 1 || v == 2) ? v : 3;
-    }
     if (algo == CDC_ALGO_FASTCDC) {
         if (min < kMinimumMin || min > kMinimumMax || avg < kAverageMin ||
             avg > kAverageMax || max < kMaximumMin || max > kMaximumMax) {
@@ -225,19 +221,12 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
         return o;
     };
     const size_t o_count = take(S * 4), o_pos = take(S * cap * 4);
-    const size_t o_st0 = take(S * smax * 8), o_nxt = take(S * cap * 8);
-    const size_t o_desc = take(S * 8), o_ent = take(S * 8), o_tk = take(16), o_stats = take(4 * 8);
+    const size_t o_starts = take(S * smax * 8);  // chunk starts beyond the LDS-resident ones
     const size_t o_first = take((N + 1) * 8);
-    // pipeline 1 state
-    const size_t o1_st1 = take(S * smax * 8), o1_ns0 = take(S * 4), o1_ns1 = take(S * 4);
-    const size_t o1_which = take(S), o1_entry = take(S * 8), o1_ex0 = take(S * 8), o1_ex1 = take(S * 8);
-    const size_t o1_changed = take(16), o1_ci = take((S + 1) * 8), o1_bs = take((S / 1024 + 2) * 8);
-    const size_t o1_stats = take((4 + N + 1) * 8);  // stats[4] ++ first[N+1]: one D2H
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
-    // pipeline 3 (fastcdc.hip) state; its chunk starts share o_st0
-    const uint64_t nb3 = p3::resolve_blocks(S) + 2;
-    const size_t o3_stats = take(p3::kStatWords * 8), o3_desc = take(6 * nb3 * 8);
-    const size_t o3_tails = take(N * 8);
+    const uint64_t nb = p3::resolve_blocks(S) + 2;
+    const size_t o_stats = take(p3::kStatWords * 8), o_desc = take(6 * nb * 8);
+    const size_t o_tails = take(N * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
     ws_spans_ = 0;
@@ -251,40 +240,17 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     cand_.cap = (uint32_t)cap;
     cand_.count = reinterpret_cast<uint32_t *>(b + o_count);
     cand_.pos = reinterpret_cast<uint32_t *>(b + o_pos);
-    chains_.smax = (uint32_t)smax;
-    chains_.starts[0] = reinterpret_cast<uint64_t *>(b + o_st0);
-    chains_.starts[1] = nullptr;
-    d_nxt_ = reinterpret_cast<uint64_t *>(b + o_nxt);
-    lb_.desc = reinterpret_cast<uint64_t *>(b + o_desc);
-    lb_.ent = reinterpret_cast<uint64_t *>(b + o_ent);
-    lb_.ticket = reinterpret_cast<uint32_t *>(b + o_tk);
-    lb_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
     d_first_ = reinterpret_cast<uint64_t *>(b + o_first);
-    chains1_.smax = (uint32_t)smax;
-    chains1_.starts[0] = chains_.starts[0];
-    chains1_.starts[1] = reinterpret_cast<uint64_t *>(b + o1_st1);
-    chains1_.nstarts[0] = reinterpret_cast<uint32_t *>(b + o1_ns0);
-    chains1_.nstarts[1] = reinterpret_cast<uint32_t *>(b + o1_ns1);
-    chains1_.which = reinterpret_cast<uint8_t *>(b + o1_which);
-    chains1_.entry = reinterpret_cast<uint64_t *>(b + o1_entry);
-    chains1_.exit[0] = reinterpret_cast<uint64_t *>(b + o1_ex0);
-    chains1_.exit[1] = reinterpret_cast<uint64_t *>(b + o1_ex1);
-    chains1_.changed = reinterpret_cast<uint32_t *>(b + o1_changed);
-    comp1_.chunk_index = reinterpret_cast<uint64_t *>(b + o1_ci);
-    comp1_.block_sums = reinterpret_cast<uint64_t *>(b + o1_bs);
-    comp1_.stats = reinterpret_cast<uint64_t *>(b + o1_stats);
-    comp1_.first = comp1_.stats + 4;
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
     ch3_.smax = (uint32_t)smax;
-    ch3_.starts = chains_.starts[0];
-    cp3_.stats = reinterpret_cast<uint64_t *>(b + o3_stats);
-    uint64_t *desc = reinterpret_cast<uint64_t *>(b + o3_desc);
-    rs3_ = p3::Resolve{desc,           desc + nb3,     desc + 2 * nb3, desc + 3 * nb3,
-                       desc + 4 * nb3, desc + 5 * nb3, 0};
-    HIP_TRY(hipMemset(desc, 0, 6 * nb3 * 8));  // no stale status word can carry a live generation
-    d_tails_ = reinterpret_cast<uint64_t *>(b + o3_tails);
+    ch3_.starts = reinterpret_cast<uint64_t *>(b + o_starts);
+    cp3_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
+    uint64_t *desc = reinterpret_cast<uint64_t *>(b + o_desc);
+    rs3_ = p3::Resolve{desc, desc + nb, desc + 2 * nb, desc + 3 * nb, desc + 4 * nb, desc + 5 * nb, 0};
+    HIP_TRY(hipMemset(desc, 0, 6 * nb * 8));  // no stale status word can carry a live generation
+    d_tails_ = reinterpret_cast<uint64_t *>(b + o_tails);
     return CDC_OK;
 }
 
@@ -336,7 +302,6 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : 0;
     uint64_t spans = 0;
     uint32_t n_tails = 0;
-    multi_span_ = false;
     for (size_t i = 0; i < n; ++i) {
         h_ptrs[i] = reinterpret_cast<uint64_t>(d_streams[i]);
         h_lens[i] = lens[i];
@@ -345,9 +310,6 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
             const uint64_t k = (lens[i] + (1ull << sl2) - 1) >> sl2;
             spans += k;
             if (lens[i] & ((1ull << sl2) - 1)) h_tails[n_tails++] = spans - 1;  // ragged last span
-            // Zero-length streams own no span, so spans > n does not imply a
-            // multi-span stream: record it per stream.
-            if (k >= 2) multi_span_ = true;
         }
     }
     h_sb[n] = spans;
@@ -386,53 +348,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     return (int64_t)first[n];
 }
 
-int Engine::run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
-                        uint64_t *first, hipStream_t s) {
-    uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats[4] ++ first[n+1]
-    HIP_TRY(hipEventRecord(ev_[0], s));
-    HIP_TRY(v1::launch_scan(st, fp_, d_gear_, cand_, num_cus_, s));
-    HIP_TRY(hipEventRecord(ev_[1], s));
-    HIP_TRY(v1::launch_trunc(st, fp_, d_gear_, cand_, s));
-    HIP_TRY(v1::launch_spec(st, fp_, d_gear_, cand_, chains1_, comp1_.stats, s));
-    int exit_buf = 0;
-    if (multi_span_) {  // some stream has >= 2 spans: chains must be joined
-        // kJacobi device passes (each a no-op once converged) and a serial
-        // catch-up that runs only if the last pass still changed an exit: no
-        // host round trip on any path.
-        for (int it = 0; it < v1::kJacobi; ++it)
-            HIP_TRY(v1::launch_fixup(st, fp_, d_gear_, cand_, chains1_, it, comp1_.stats, s));
-        exit_buf = v1::kJacobi & 1;
-        HIP_TRY(v1::launch_serial(st, fp_, d_gear_, cand_, chains1_, exit_buf, (v1::kJacobi - 1) % 3,
-                                  comp1_.stats, s));
-    }
-    HIP_TRY(hipEventRecord(ev_[2], s));
-    HIP_TRY(v1::launch_compact(st, chains1_, exit_buf, cand_, comp1_, d_out, s));
-    HIP_TRY(hipMemcpyAsync(h_misc, comp1_.stats, (4 + n + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(ev_[3], s));
-    HIP_TRY(hipStreamSynchronize(s));
-    // Zero-length streams own no span: their first[] is the next stream's.
-    const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
-    uint64_t *hf = h_misc + 4;
-    for (size_t i = n; i-- > 0;)
-        if (lens[i] == 0) hf[i] = hf[i + 1];
-    std::memcpy(first, hf, (n + 1) * 8);
-    float t01 = 0, t12 = 0, t23 = 0, t03 = 0;
-    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
-    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
-    HIP_TRY(hipEventElapsedTime(&t23, ev_[2], ev_[3]));
-    HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
-    timing_.scan_ms = t01;
-    timing_.resolve_ms = t12;
-    timing_.compact_ms = t23;
-    timing_.total_ms = t03;
-    timing_.candidates = h_misc[0];
-    timing_.overflow_spans = (uint32_t)h_misc[1];
-    timing_.fixup_iterations = (uint32_t)h_misc[2] + (h_misc[3] ? 1000u : 0u);
-    return CDC_OK;
-}
-
-int Engine::run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
+int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                         uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats ++ first[n+1], written by the device
@@ -478,48 +394,6 @@ int Engine::run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
     timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk];
     timing_.walk_fallback_steps = h_misc[p3::kStatOnDemand];
-    return CDC_OK;
-}
-
-int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
-                     uint64_t *first, hipStream_t s) {
-    if (pipeline_ == 3) return run_fast_v3(st, d_out, n, first, s);
-    if (pipeline_ == 1) return run_fast_v1(st, d_out, n, first, s);
-    uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats[4] ++ first[n+1], written by the device
-    Lookback lb = lb_;
-    lb.h_stats = h_misc;
-    lb.h_first = h_misc + 4;
-    h_misc[3] = ~0ull;  // sentinel: overwritten by the resolve kernel's last workgroup
-    HIP_TRY(hipEventRecord(ev_[0], s));
-    HIP_TRY(launch_scan(st, fp_, d_gear_, cand_, lb, num_cus_, s));
-    HIP_TRY(hipEventRecord(ev_[1], s));
-    HIP_TRY(launch_next(st, fp_, d_gear_, cand_, d_nxt_, s));
-    HIP_TRY(launch_resolve(st, fp_, d_gear_, cand_, d_nxt_, chains_, lb, d_out, out_cap_, s));
-    HIP_TRY(hipEventRecord(ev_[2], s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (h_misc[3] != 0) {
-        set_error(h_misc[3] == ~0ull ? "resolve kernel did not report back"
-                                     : "resolve look-back timed out or chain overflowed (internal error)");
-        return CDC_EDEVICE;
-    }
-    // Zero-length streams own no span: their first[] is the next stream's.
-    const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
-    uint64_t *hf = h_misc + 4;
-    for (size_t i = n; i-- > 0;)
-        if (lens[i] == 0) hf[i] = hf[i + 1];
-    std::memcpy(first, hf, (n + 1) * 8);
-    float t01 = 0, t12 = 0, t02 = 0;
-    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
-    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
-    HIP_TRY(hipEventElapsedTime(&t02, ev_[0], ev_[2]));
-    timing_.scan_ms = t01;
-    timing_.resolve_ms = t12;
-    timing_.compact_ms = 0;  // fused into the resolve kernel
-    timing_.total_ms = t02;
-    timing_.candidates = h_misc[0];
-    timing_.overflow_spans = (uint32_t)h_misc[1];
-    timing_.fixup_iterations = (uint32_t)h_misc[2];
     return CDC_OK;
 }
 
@@ -664,9 +538,6 @@ int64_t Engine::debug_copy(int what, void *out, size_t max_bytes) {
     } else if (what == 1) {
         src = cand_.pos;
         bytes = last_spans_ * cap_ * 4;
-    } else if (what == 2) {
-        src = d_nxt_;
-        bytes = last_spans_ * cap_ * 8;
     } else {
         set_error("debug_copy: unknown array");
         return CDC_EINVAL;

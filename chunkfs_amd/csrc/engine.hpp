@@ -13,7 +13,6 @@
 #include "../../include/chunkfs_amd.h"
 #include "cdc_kernels.hpp"
 #include "fastcdc.hpp"
-#include "pipeline_v1.hpp"
 
 namespace cdc {
 
@@ -57,11 +56,10 @@ class Engine {
     int fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s);
     // Debug (include/chunkfs_amd_debug.h): copy an intermediate array of the
     // last FastCDC batch to the host.  what: 0 = per-span candidate counts
-    // (u32), 1 = candidate records (u32, cap per span), 2 = record links of
-    // pipeline 2 (u64, cap per span).  Returns bytes copied.
+    // (u32), 1 = candidate records (u32, cap per span).  Returns bytes copied.
     int64_t debug_copy(int what, void *out, size_t max_bytes);
     uint32_t record_cap() const { return cap_; }
-    int pipeline() const { return pipeline_; }
+    int pipeline() const { return 3; }  // (one FastCDC pipeline: scan + resolve)
 
   private:
     Engine() = default;
@@ -70,10 +68,6 @@ class Engine {
     int ensure_host_staging(size_t n);
     int run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                  uint64_t *first, hipStream_t s);
-    int run_fast_v1(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
-                    uint64_t *first, hipStream_t s);
-    int run_fast_v3(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
-                    uint64_t *first, hipStream_t s);
     int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                   cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
 
@@ -82,10 +76,6 @@ class Engine {
     int device_ = 0;
     int num_cus_ = 256;
     FastParams fp_{};
-    // FastCDC pipeline: 1 = pipeline_v1.hip (GPU-validated, default), 2 =
-    // cdc_kernels.hip (per-lane sub-span scan, record links + lane walk);
-    // environment CHUNKFS_AMD_PIPELINE at cdc_create.
-    int pipeline_ = 3;
     uint32_t span_log2_ = 16;
     uint32_t cap_ = 0, smax_ = 0;
     std::string describe_;
@@ -100,24 +90,19 @@ class Engine {
     uint64_t ws_spans_ = 0;
     size_t ws_streams_ = 0;
     Candidates cand_{};
-    Chains chains_{};
-    Lookback lb_{};
-    v1::Chains chains1_{};         // pipeline 1 (pipeline_v1.hip)
-    v1::Compact comp1_{};
-    p3::Chains ch3_{};             // pipeline 3 (fastcdc.hip, default)
+    p3::Chains ch3_{};             // chunk starts spilled past the resolve's LDS
     p3::Compact cp3_{};
     p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
     uint64_t res_gen_ = 0;
     uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids
     uint32_t n_tails_ = 0;
-    uint64_t *d_nxt_ = nullptr;    // [spans*cap] record links (next_kernel)
     uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
     const uint8_t **d_ptrs_ = nullptr;
     uint64_t *d_lens_ = nullptr;
     uint64_t *d_span_base_ = nullptr;
 
     // Pinned, device-visible (coherent) host staging: the small per-call
-    // tables going in, stats[4] ++ first[n+1] coming back (written by the
+    // tables going in, stats ++ first[n+1] coming back (written by the
     // resolve kernel directly, no copy).
     void *h_stage_ = nullptr;
     size_t h_stage_streams_ = 0;
@@ -138,8 +123,7 @@ class Engine {
     std::vector<uint64_t> tables_;
     uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
     uint64_t last_spans_ = 0;  // spans of the last FastCDC batch (debug_copy)
-    uint64_t out_cap_ = 0;     // capacity of the current batch's output (walk_kernel bound)
-    bool multi_span_ = false;  // some stream of the current batch has >= 2 spans
+    uint64_t out_cap_ = 0;     // capacity of the current batch's output (resolve bound)
 };
 
 void set_error(const std::string &msg);

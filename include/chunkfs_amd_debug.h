@@ -13,7 +13,7 @@
 extern "C" {
 #endif
 
-/* FastCDC pipeline of the handle: 1 (pipeline_v1.hip) or 2 (cdc_kernels.hip). */
+/* FastCDC pipeline of the handle: 3 (fastcdc.hip: scan + resolve), the only one. */
 int cdc_debug_pipeline(const cdc_handle_t *h);
 /* Candidate-record capacity per span (records are stored `cap` per span). */
 uint32_t cdc_debug_record_cap(const cdc_handle_t *h);

@@ -26,10 +26,9 @@ _cache = {}
 
 def chunker(sizes):
     import chunkfs_amd as c
-    key = (sizes, os.environ.get("CHUNKFS_AMD_PIPELINE", "1"))
-    if key not in _cache:
-        _cache[key] = c.FastChunker(c.SizeParams(*sizes))
-    return _cache[key]
+    if sizes not in _cache:
+        _cache[sizes] = c.FastChunker(c.SizeParams(*sizes))
+    return _cache[sizes]
 
 
 def assert_same(gpu, ref, what=""):

@@ -3,9 +3,9 @@ checked against the sequential oracle on the CPU.
 
 The GPU replaces the reference's sequential cut loop (fastcdc v2020
 `cut_gear`) by: a windowed-hash candidate scan; per-record
-links to the next chunk start (next_kernel); per-span speculative chain walks
-from a 2*max warm-up start, settled against the previous span's exit
-(walk_kernel).  This model restates those steps in numpy/Python with the same
+links to the next chunk start; per-span speculative chain walks from a
+warm-up start, settled against the previous span's exit (fastcdc.hip
+resolve_kernel).  This model restates those steps in numpy/Python with the same
 span size, warm-up, regime and record semantics, so a flaw in the
 decomposition itself (not in its HIP code) shows up here, on CPU.
 """
@@ -62,7 +62,7 @@ class Model:
         self.nxt = {}
 
     def step(self, s):
-        """Start of the chunk after the one starting at s (lane_next / next_kernel)."""
+        """Start of the chunk after the one starting at s (an exact step)."""
         n = self.n
         if n - s <= self.mn:
             return n
@@ -84,7 +84,7 @@ class Model:
         return s + rem
 
     def link(self, s):
-        """next_kernel's precomputed link when s is a record, else a lane step."""
+        """the precomputed link when s is a record, else a lane step."""
         if s in self.idx:
             if s not in self.nxt:
                 self.nxt[s] = self.step(s)
