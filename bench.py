@@ -63,6 +63,8 @@ def parse(argv=None):
     p.add_argument("--no-parity", action="store_true", help="skip the one-off oracle check")
     p.add_argument("--no-sweep", action="store_true",
                    help="skip the avg 4/16 KiB and low-entropy lines (N=1)")
+    p.add_argument("--no-algos", action="store_true",
+                   help="skip the Rabin / Ultra / Leap / Seq lines (N=1)")
     p.add_argument("--hash", action="store_true", help="also report the SHA-256 fingerprint rate (§8f row 2)")
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the one-off host-buffer (PCIe-inclusive) rates")
@@ -279,6 +281,56 @@ def sweep_lines(args, eng, steps):
     return res
 
 
+def algo_lines(args, eng, steps):
+    """Rabin / UltraCDC / LeapCDC / SeqCDC (segment-walk engine) over the same
+    1 GiB stream at the bench sizes: device GiB/s, the walk / fix-up split,
+    bit-exactness against the oracle on the whole stream, and the oracle's
+    single-thread rate on the same bytes (parity vs the crate is unpinned)."""
+    import numpy as np
+    import torch
+    import chunkfs_amd as cfa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n = eng.lens[0]
+    buf = eng.bufs[0]
+    sizes = cfa.SizeParams(args.min, args.avg, args.max)
+    host = buf[:n].cpu().numpy() if not args.no_parity else None
+    res = {}
+    for name in ("rabin", "ultra", "leap", "seq"):
+        ch = {"rabin": cfa.RabinChunker, "ultra": cfa.UltraChunker, "leap": cfa.LeapChunker}.get(name)
+        ch = ch(sizes, device=eng.local) if ch else cfa.SeqChunker(cfa.OperationMode.Increasing, sizes,
+                                                                  device=eng.local)
+        cap = ch.batch_max_chunks([n])
+        out = torch.empty((cap, 2), dtype=torch.int64, device=eng.dev)
+        first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+        torch.cuda.synchronize()
+        walk, tot, rew = [], [], []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+            t = ch.last_timing()
+            walk.append(t["scan_ms"])
+            tot.append(t["total_ms"])
+            rew.append(t["fixup_iterations"])
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        line = {"sizes": [args.min, args.avg, args.max], "GiBps": n * steps / el / (1 << 30),
+                "ms_per_step": el / steps * 1e3, "walk_ms": sum(walk) / len(walk),
+                "device_total_ms": sum(tot) / len(tot), "rewalked_segments": max(rew), "chunks": int(first[1]),
+                "frac_of_hbm": n * steps / el / 1e9 / HBM_PEAK_GBS}
+        if host is not None:
+            got = out[:int(first[1])].cpu().numpy().view(np.uint64)
+            secs = time.perf_counter()
+            ref = oracle.cdc(name, host, args.min, args.avg, args.max)
+            secs = time.perf_counter() - secs
+            line["parity_vs_oracle"] = bool(got.shape == ref.shape and (got == ref).all())
+            line["cpu_single_thread_GiBps"] = n / secs / (1 << 30)
+        res[name] = line
+        ch.close()
+        del out
+    return res
+
+
 def host_path_leg(eng):
     """PCIe-inclusive rates of the host boundary, recorded beside `value`,
     never as it: cdc_chunk_data on a 1 GiB host buffer, and the
@@ -398,6 +450,8 @@ def main(argv=None):
             extras["parity_streams_checked"] = len(checked)
         if not args.no_sweep and args.workload == "stream":
             extras["sweep"] = sweep_lines(args, eng, max(5, args.steps // 2))
+        if not args.no_algos and args.workload == "stream":
+            extras["other_chunkers"] = algo_lines(args, eng, 3)
         if args.cpu_seconds > 0:
             extras["cpu_baseline"] = cpu_baseline_leg(args, eng.bufs[0][:shard.lens[0]].cpu().numpy())
             fw = extras.get("host_path", {}).get("fs_write_1MiB_segments")

@@ -9,8 +9,10 @@ include/chunkfs_amd.h (libchunkfs_amd.so, hand-written HIP for gfx950):
     SizeParams       src/chunkers/mod.rs:1    SizeParams
     FastChunker      src/chunkers/fast.rs     FastChunker
     FSChunker        src/chunkers/fixed_size  FSChunker
-    Rabin/Super/Ultra/Leap/Seq                raise NotImplementedError (no oracle
-                                              offline: cdc-chunkers 0.1.3 absent)
+    Rabin/Ultra/Leap/Seq src/chunkers/*.rs    RabinChunker, UltraChunker, LeapChunker,
+                                              SeqChunker (published algorithms; parity
+                                              unpinned: cdc-chunkers 0.1.3 absent)
+    SuperChunker                              raises NotImplementedError
     ChunkStorage::write  system/storage.rs    write_spans()
 
 Every call runs on the GPU.  There is no CPU fallback: without the built
@@ -31,7 +33,7 @@ SEG_SIZE = MB  # src/lib.rs:39
 __all__ = [
     "KB", "MB", "GB", "SEG_SIZE", "Chunk", "SizeParams", "Chunker", "FastChunker",
     "FSChunker", "RabinChunker", "SuperChunker", "UltraChunker", "LeapChunker",
-    "SeqChunker", "CdcError", "write_spans", "version",
+    "SeqChunker", "OperationMode", "SeqConfig", "CdcError", "write_spans", "version",
 ]
 
 
@@ -226,23 +228,89 @@ class FSChunker(Chunker):
         return cls()
 
 
-def _unsupported(name, algo):
-    class _C(Chunker):
-        def __init__(self, sizes=None, device=0):
-            s = sizes or SizeParams(2 * KB, 8 * KB, 64 * KB)
-            super().__init__(algo, s.min, s.avg, s.max, device)
+class _SizedChunker(Chunker):
+    """Common constructor of the chunkers built on the segment-walk engine.
 
-    _C.__name__ = name
-    _C.__doc__ = (f"{name} (src/chunkers/{algo}.rs): not implemented -- its arithmetic lives in "
-                  "cdc-chunkers 0.1.3, absent offline, so no oracle exists (SURVEY.md §8c).")
-    return _C
+    The reference's Default sizes (SizeParams::{rabin,ultra,leap,seq}_default)
+    live in cdc-chunkers 0.1.3, absent offline, so sizes are always explicit.
+    Cut rules restate the published algorithms: parity unpinned."""
+
+    _name = None
+
+    def __init__(self, sizes, device=0):
+        if sizes is None:
+            raise TypeError(f"{self._name}: pass SizeParams explicitly (the crate's defaults are unknown here)")
+        self.sizes = sizes
+        super().__init__(self._algo, sizes.min, sizes.avg, sizes.max, device)
 
 
-RabinChunker = _unsupported("RabinChunker", "rabin")
-SuperChunker = _unsupported("SuperChunker", "super")
-UltraChunker = _unsupported("UltraChunker", "ultra")
-LeapChunker = _unsupported("LeapChunker", "leap")
-SeqChunker = _unsupported("SeqChunker", "seq")
+class RabinChunker(_SizedChunker):
+    """Rabin CDC (src/chunkers/rabin.rs:34-56): 48-byte window fingerprint modulo
+    a degree-53 polynomial, cut where digest & (2^round(log2 avg) - 1) == 0."""
+    _algo, _name = "rabin", "RabinChunker"
+
+
+class UltraChunker(_SizedChunker):
+    """UltraCDC (src/chunkers/ultra.rs:30-44): 8-byte Hamming distance to 0xAA..,
+    two masks around the normal size, low-entropy (LEST) early cut."""
+    _algo, _name = "ultra", "UltraChunker"
+
+
+class LeapChunker(_SizedChunker):
+    """Leap-based CDC (src/chunkers/leap.rs:30-44): 24 eligible windows before a
+    cut, leaping past a failing window."""
+    _algo, _name = "leap", "LeapChunker"
+
+
+class OperationMode:
+    """seq::OperationMode (re-exported at src/chunkers/seq.rs:3)."""
+    Increasing = 0
+    Decreasing = 1
+
+
+class SeqConfig:
+    """seq::Config (re-exported at src/chunkers/seq.rs:3); defaults of
+    include/chunkfs_amd_cdc_params.h (the crate's field names are unknown)."""
+
+    __slots__ = ("seq_length", "jump_trigger", "jump_size")
+
+    def __init__(self, seq_length=5, jump_trigger=50, jump_size=256):
+        self.seq_length, self.jump_trigger, self.jump_size = int(seq_length), int(jump_trigger), int(jump_size)
+
+    def __repr__(self):
+        return (f"Config {{ seq_length: {self.seq_length}, jump_trigger: {self.jump_trigger}, "
+                f"jump_size: {self.jump_size} }}")
+
+
+class SeqChunker(Chunker):
+    """SeqCDC (src/chunkers/seq.rs:40-55): SeqChunker::new(mode, sizes, config).
+    estimate_chunk_count is len / avg (seq.rs:52-54), unlike the others."""
+
+    _algo = "seq"
+
+    def __init__(self, mode=OperationMode.Increasing, sizes=None, config=None, device=0):
+        if sizes is None:
+            raise TypeError("SeqChunker: pass SizeParams explicitly (the crate's defaults are unknown here)")
+        self.mode, self.sizes = int(mode), sizes
+        self.config = config or SeqConfig()
+        L = lib()
+        h = ctypes.c_void_p()
+        check(L.cdc_create_seq(self.mode, self.config.seq_length, self.config.jump_trigger,
+                               self.config.jump_size, sizes.min, sizes.avg, sizes.max, device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+
+class SuperChunker(Chunker):
+    """SuperCDC (src/chunkers/supercdc.rs:35-57): NOT implemented.  Its cut rule
+    and the cross-call `records` map live in cdc-chunkers 0.1.3, absent offline;
+    the constructor raises NotImplementedError (CDC_ENOTSUP)."""
+
+    _algo = "super"
+
+    def __init__(self, sizes=None, device=0):
+        s = sizes or SizeParams(2 * KB, 8 * KB, 64 * KB)
+        super().__init__("super", s.min, s.avg, s.max, device)
 
 
 def write_spans(chunker, data, seg_size=SEG_SIZE):

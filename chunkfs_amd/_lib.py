@@ -19,7 +19,7 @@ ALGO = {"fast": 0, "fixed": 1, "rabin": 2, "super": 3, "ultra": 4, "leap": 5, "s
 
 # Every symbol include/chunkfs_amd.h declares (tests check the export table).
 EXPORTS = [
-    "cdc_create", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
+    "cdc_create", "cdc_create_seq", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
     "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear",
     "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
     "cdc_fs_write", "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
@@ -92,6 +92,9 @@ def lib():
     L.cdc_create.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                              ctypes.c_int, ctypes.POINTER(P)]
     L.cdc_create.restype = ctypes.c_int
+    u32 = ctypes.c_uint32
+    L.cdc_create_seq.argtypes = [u32, u32, u32, u32, u32, u32, u32, ctypes.c_int, ctypes.POINTER(P)]
+    L.cdc_create_seq.restype = ctypes.c_int
     L.cdc_destroy.argtypes = [P]
     L.cdc_destroy.restype = None
     L.cdc_chunk_data.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), sz]

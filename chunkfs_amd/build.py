@@ -11,8 +11,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libchunkfs_amd.so")
-SOURCES = ["fastcdc.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "capi.cpp", "index_host.cpp"]
-HEADERS = ["fastcdc.hpp", "cdc_kernels.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
+SOURCES = ["fastcdc.hip", "walk.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "capi.cpp", "index_host.cpp"]
+HEADERS = ["fastcdc.hpp", "walk.hpp", "cdc_kernels.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
@@ -24,7 +24,7 @@ def source_digest():
     import hashlib
     h = hashlib.sha256()
     files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [
-        os.path.join(ROOT, "include", f) for f in ("chunkfs_amd.h", "chunkfs_amd_tables.h", "chunkfs_amd_debug.h")]
+        os.path.join(ROOT, "include", f) for f in ("chunkfs_amd.h", "chunkfs_amd_tables.h", "chunkfs_amd_debug.h", "chunkfs_amd_cdc_params.h")]
     for f in files:
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
@@ -50,6 +50,7 @@ def build(force=False):
         os.path.join(ROOT, "include", "chunkfs_amd.h"),
         os.path.join(ROOT, "include", "chunkfs_amd_tables.h"),
         os.path.join(ROOT, "include", "chunkfs_amd_debug.h"),
+        os.path.join(ROOT, "include", "chunkfs_amd_cdc_params.h"),
     ]
     objs = []
     for src in SOURCES:

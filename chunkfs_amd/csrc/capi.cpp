@@ -28,6 +28,16 @@ int cdc_create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
     return CDC_OK;
 }
 
+int cdc_create_seq(uint32_t mode, uint32_t seq_length, uint32_t jump_trigger, uint32_t jump_size,
+                   uint32_t min, uint32_t avg, uint32_t max, int device, cdc_handle_t **out) {
+    const uint32_t cfg[4] = {mode, seq_length, jump_trigger, jump_size};
+    cdc::Engine *e = nullptr;
+    const int rc = cdc::Engine::create_seq(cfg, min, avg, max, device, &e);
+    if (rc != CDC_OK) return rc;
+    *out = new cdc_handle{e};
+    return CDC_OK;
+}
+
 void cdc_destroy(cdc_handle_t *h) {
     if (!h) return;
     delete h->engine;

@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "../../include/chunkfs_amd_cdc_params.h"
 #include "../../include/chunkfs_amd_tables.h"
 #include "fastcdc.hpp"
 #include "sha256.hpp"
@@ -58,9 +59,13 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         return CDC_EINVAL;
     }
     *out = nullptr;
+    if (algo == CDC_ALGO_RABIN || algo == CDC_ALGO_ULTRA || algo == CDC_ALGO_LEAP || algo == CDC_ALGO_SEQ) {
+        const uint32_t seq[4] = {0, CDC_SEQ_LENGTH, CDC_SEQ_JUMP_TRIGGER, CDC_SEQ_JUMP_SIZE};
+        return create_walk(algo, seq, min, avg, max, device, out);
+    }
     if (algo != CDC_ALGO_FASTCDC && algo != CDC_ALGO_FIXED) {
-        set_error("algorithm not implemented on MI355X: its reference arithmetic "
-                  "lives in cdc-chunkers 0.1.3, absent offline (SURVEY.md §8c)");
+        set_error("SuperCDC is not implemented on MI355X: its chunk records (supercdc.rs:10, 37-50) "
+                  "follow cdc-chunkers 0.1.3, absent offline (SURVEY.md §8c)");
         return CDC_ENOTSUP;
     }
     Engine *e = new Engine();
@@ -169,6 +174,8 @@ Engine::~Engine() {
     (void)hipFree(d_out_);
     (void)hipFree(d_dig_);
     (void)hipFree(d_counter_);
+    (void)hipFree(d_wtabs_);
+    (void)hipFree(wws_);
     (void)hipHostFree(h_stage_);
     for (auto &ev : ev_)
         if (ev) (void)hipEventDestroy(ev);
@@ -187,7 +194,8 @@ int Engine::set_gear(const uint64_t *gear) {
 
 size_t Engine::estimate(size_t len) const {
     if (algo_ == CDC_ALGO_FIXED) return len / min_ + 1;  // fixed_size.rs:45-47
-    return len / min_;                                   // fast.rs:47-49
+    if (algo_ == CDC_ALGO_SEQ) return len / avg_;        // seq.rs:52-54
+    return len / min_;  // fast.rs:47-49, rabin.rs:53-55, ultra.rs:41-43, leap.rs:41-43
 }
 
 size_t Engine::batch_max_chunks(size_t n, const uint64_t *lens) const {
@@ -299,7 +307,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
     uint64_t *h_tails = h + 3 * h_stage_streams_;
-    const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : 0;
+    const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : is_walk() ? seg_log2_ : 0;
     uint64_t spans = 0;
     uint32_t n_tails = 0;
     for (size_t i = 0; i < n; ++i) {
@@ -310,14 +318,16 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
             const uint64_t k = (lens[i] + (1ull << sl2) - 1) >> sl2;
             spans += k;
             if (lens[i] & ((1ull << sl2) - 1)) h_tails[n_tails++] = spans - 1;  // ragged last span
+        } else if (is_walk()) {
+            spans += (lens[i] + (1ull << sl2) - 1) >> sl2;  // segments
         }
     }
     h_sb[n] = spans;
-    if (algo_ == CDC_ALGO_FASTCDC && spans == 0) {  // every stream is empty
+    if (algo_ != CDC_ALGO_FIXED && spans == 0) {  // every stream is empty
         for (size_t i = 0; i <= n; ++i) first[i] = 0;
         return 0;
     }
-    rc = ensure_workspace(spans, n);
+    rc = is_walk() ? ensure_walk_workspace(spans, n) : ensure_workspace(spans, n);
     if (rc) return rc;
     // The three per-stream tables are re-uploaded only when they change
     // (repeated batches over the same device buffers skip the H2D copies).
@@ -343,6 +353,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     last_spans_ = algo_ == CDC_ALGO_FASTCDC ? spans : 0;
     n_tails_ = n_tails;
     rc = algo_ == CDC_ALGO_FASTCDC ? run_fast(st, d_out, n, first, s)
+         : is_walk()               ? run_walk(st, d_out, n, first, s)
                                    : run_fixed(st, n, lens, d_out, first, s);
     if (rc) return rc;
     return (int64_t)first[n];
@@ -554,6 +565,217 @@ int Engine::fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream
     hipStream_t st = s ? s : own_stream_;
     HIP_TRY(launch_fill_splitmix64(d_buf, len, seed, st));
     HIP_TRY(hipStreamSynchronize(st));
+    return CDC_OK;
+}
+
+// ---- Rabin / UltraCDC / LeapCDC / SeqCDC: the segment-walk engine ----------
+
+namespace {
+// GF(2) remainder modulo the Rabin polynomial (host-side table build).
+uint64_t gf2_mod(uint64_t x, uint64_t p) {
+    const int dp = 63 - __builtin_clzll(p);
+    while (x) {
+        const int dx = 63 - __builtin_clzll(x);
+        if (dx < dp) break;
+        x ^= p << (dx - dp);
+    }
+    return x;
+}
+
+uint64_t splitmix_word(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+}  // namespace
+
+int Engine::create_seq(const uint32_t seq[4], uint32_t min, uint32_t avg, uint32_t max, int device,
+                       Engine **out) {
+    if (!seq) {
+        set_error("cdc_create_seq: config is NULL");
+        return CDC_EINVAL;
+    }
+    return create_walk(CDC_ALGO_SEQ, seq, min, avg, max, device, out);
+}
+
+int Engine::create_walk(cdc_algo_t algo, const uint32_t seq[4], uint32_t min, uint32_t avg, uint32_t max,
+                        int device, Engine **out) {
+    if (!out) {
+        set_error("cdc_create: out is NULL");
+        return CDC_EINVAL;
+    }
+    *out = nullptr;
+    // Size rules (oracle_cdc_check): 0 < min <= avg <= max, and the
+    // bytes each rule reads before the first tested position.
+    if (min == 0 || min > avg || avg > max || (algo == CDC_ALGO_ULTRA && min < 8) ||
+        (algo == CDC_ALGO_LEAP && min < 32) || (algo == CDC_ALGO_RABIN && avg < 2)) {
+        set_error("invalid sizes: need 0 < min <= avg <= max (UltraCDC min >= 8, LeapCDC min >= 32)");
+        return CDC_EINVAL;
+    }
+    if (algo == CDC_ALGO_SEQ && (seq[0] > 1 || seq[1] == 0 || seq[2] == 0)) {
+        set_error("invalid SeqCDC config: mode 0/1, seq_length > 0, jump_trigger > 0");
+        return CDC_EINVAL;
+    }
+    Engine *e = new Engine();
+    e->algo_ = algo;
+    e->min_ = min;
+    e->avg_ = avg;
+    e->max_ = max;
+    e->device_ = device;
+    const char *name = algo == CDC_ALGO_RABIN ? "RabinCDC" : algo == CDC_ALGO_ULTRA ? "UltraCDC"
+                     : algo == CDC_ALGO_LEAP ? "LeapCDC" : "SeqCDC";
+    char buf[256];
+    // impl Debug (rabin.rs:28-32, ultra.rs:24-28, leap.rs:24-28, seq.rs:34-38)
+    if (algo == CDC_ALGO_SEQ)
+        std::snprintf(buf, sizeof buf, "%s, sizes: SizeParams { min: %u, avg: %u, max: %u }, mode: %s [MI355X gfx950]",
+                      name, min, avg, max, seq[0] ? "Decreasing" : "Increasing");
+    else
+        std::snprintf(buf, sizeof buf, "%s, sizes: SizeParams { min: %u, avg: %u, max: %u } [MI355X gfx950]", name,
+                      min, avg, max);
+    e->describe_ = buf;
+    int rc = e->init();
+    if (rc == CDC_OK) rc = e->init_walk(seq);
+    if (rc != CDC_OK) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return CDC_OK;
+}
+
+int Engine::init_walk(const uint32_t *seq) {
+    walk::WalkParams &wp = wp_;
+    wp.algo = (uint32_t)algo_;
+    wp.min = min_;
+    wp.avg = avg_;
+    wp.max = max_;
+    wp.rabin_mask = (1ull << cdc_log2_round(avg_)) - 1;
+    wp.rabin_shift = (uint32_t)(63 - __builtin_clzll(CDC_RABIN_POLY)) - 8;
+    const uint64_t lspan = avg_ > min_ ? (uint64_t)(avg_ - min_) : 1;
+    const uint32_t lb = cdc_log2_round(lspan);
+    wp.leap_thr = CDC_LEAP_THRESHOLD[lb > 32 ? 32 : lb];
+    wp.seq_mode = seq[0];
+    wp.seq_len = seq[1];
+    wp.seq_trig = seq[2];
+    wp.seq_jump = seq[3];
+    // Segments of 2^seg_log2 bytes (one lane each) and a warm-up of `warm`
+    // bytes; CHUNKFS_AMD_WALK="seg_log2,warm_over_max" overrides (experiments).
+    // Defaults (tools/walk_bench.py sweeps on MI355X): segments of
+    // >= 2 max and >= 32 KiB, a warm-up of 4 max (a chain from an arbitrary
+    // start merges with the true one within a few chunks).
+    const uint32_t l2 = ceil_log2(max_) + 1;
+    seg_log2_ = l2 < 15 ? 15 : l2;
+    uint64_t warm_mult = 4;
+    if (const char *w = std::getenv("CHUNKFS_AMD_WALK")) {
+        unsigned a = 0, b = 0;
+        if (std::sscanf(w, "%u,%u", &a, &b) == 2 && a >= 10 && a <= 30) {
+            seg_log2_ = a;
+            warm_mult = b;
+        }
+    }
+    wp.warm = warm_mult * max_;
+    wp.cap = (uint32_t)((1ull << seg_log2_) / min_ + 2);
+    // Tables: Rabin mod/out (appending a byte; sliding one out of the window),
+    // LeapCDC window-hash table.
+    uint64_t t[768];
+    const uint64_t P = CDC_RABIN_POLY;
+    const int deg = 63 - __builtin_clzll(P);
+    for (uint64_t b = 0; b < 256; ++b) {
+        t[b] = gf2_mod(b << deg, P) | (b << deg);
+        uint64_t h = b;
+        for (uint32_t i = 1; i < CDC_RABIN_WINDOW; ++i) h = gf2_mod(h << 8, P);
+        t[256 + b] = h;
+        t[512 + b] = splitmix_word(CDC_LEAP_SEED + (b + 1) * 0x9E3779B97F4A7C15ull);
+    }
+    HIP_TRY(hipMalloc(&d_wtabs_, sizeof t));
+    HIP_TRY(hipMemcpy(d_wtabs_, t, sizeof t, hipMemcpyHostToDevice));
+    wp.tabs = d_wtabs_;
+    return CDC_OK;
+}
+
+int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
+    if (wws_ && segs <= wws_segs_ && n <= wws_streams_) return CDC_OK;
+    const uint64_t S = segs > wws_segs_ ? segs + segs / 4 + 16 : wws_segs_;
+    const size_t N = n > wws_streams_ ? n + 64 : wws_streams_;
+    const uint64_t nb = S / walk::kScanBlock + 2;
+    const size_t A = 256;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = align_up(off + bytes, A);
+        return o;
+    };
+    const size_t oE = take(S * 8), oX = take(S * 8), oXs = take(S * 8), oP = take((S + 1) * 8);
+    const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
+    const size_t oF = take((N + 1) * 8), oG = take(4 * 8);
+    const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
+    (void)hipFree(wws_);
+    wws_ = nullptr;
+    wws_segs_ = 0;
+    wws_streams_ = 0;
+    HIP_TRY(hipMalloc(&wws_, off));
+    ++ws_gen_;  // the stream tables move: re-upload them
+    wws_segs_ = S;
+    wws_streams_ = N;
+    char *b = static_cast<char *>(wws_);
+    wst_.E = reinterpret_cast<uint64_t *>(b + oE);
+    wst_.X = reinterpret_cast<uint64_t *>(b + oX);
+    wst_.Xs = reinterpret_cast<uint64_t *>(b + oXs);
+    wst_.P = reinterpret_cast<uint64_t *>(b + oP);
+    wst_.N = reinterpret_cast<uint32_t *>(b + oN);
+    wst_.list = reinterpret_cast<uint64_t *>(b + oL);
+    wst_.bsum = reinterpret_cast<uint64_t *>(b + oB);
+    wst_.first = reinterpret_cast<uint64_t *>(b + oF);
+    wst_.flags = reinterpret_cast<unsigned long long *>(b + oG);
+    d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
+    d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
+    d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
+    return CDC_OK;
+}
+
+int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64_t *first, hipStream_t s) {
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_flags = h + 4 * h_stage_streams_;  // flags[4] ++ first[n+1]
+    uint64_t *h_first = h_flags + 4;
+    HIP_TRY(hipMemsetAsync(wst_.flags, 0, 4 * 8, s));
+    HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(walk::launch_walk(st, wp_, wst_, s));
+    HIP_TRY(hipEventRecord(ev_[1], s));
+    // Jacobi rounds: re-walk every segment whose entry is not its predecessor's
+    // exit, until none is (normally the first round finds none).
+    uint64_t rewalked = 0;
+    bool settled = false;
+    for (uint32_t r = 0; r < max_rounds_ && !settled; ++r) {
+        HIP_TRY(hipMemsetAsync(wst_.flags, 0, 8, s));         // segments re-walked
+        HIP_TRY(hipMemsetAsync(wst_.flags + 2, 0xFF, 8, s));  // lowest re-walked segment
+        HIP_TRY(walk::launch_fix(st, wp_, wst_, s));
+        HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        rewalked += h_flags[0];
+        settled = h_flags[0] == 0;
+    }
+    // Chains that never merge (periodic data): one exact in-order pass from
+    // the lowest segment the last round changed.
+    if (!settled) HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
+    HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
+    HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ev_[2], s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h_flags[1] != 0) {
+        set_error("segment walk: chunk list or output bound exceeded (internal error)");
+        return CDC_EDEVICE;
+    }
+    std::memcpy(first, h_first, (n + 1) * 8);
+    float t01 = 0, t12 = 0, t02 = 0;
+    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
+    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
+    HIP_TRY(hipEventElapsedTime(&t02, ev_[0], ev_[2]));
+    timing_.scan_ms = t01;
+    timing_.resolve_ms = t12;
+    timing_.total_ms = t02;
+    timing_.fixup_iterations = (uint32_t)rewalked;
+    timing_.overflow_spans = settled ? 0u : 1u;
     return CDC_OK;
 }
 

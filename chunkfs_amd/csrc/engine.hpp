@@ -13,6 +13,7 @@
 #include "../../include/chunkfs_amd.h"
 #include "cdc_kernels.hpp"
 #include "fastcdc.hpp"
+#include "walk.hpp"
 
 namespace cdc {
 
@@ -21,6 +22,10 @@ class Engine {
     // Returns CDC_OK or a negative CDC_E* code (message via set_error()).
     static int create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
                       int device, Engine **out);
+    // SeqChunker::new(mode, sizes, config) (seq.rs:16-24): seq = {mode,
+    // seq_length, jump_trigger, jump_size} (mode 0 increasing, 1 decreasing).
+    static int create_seq(const uint32_t seq[4], uint32_t min, uint32_t avg, uint32_t max,
+                          int device, Engine **out);
     ~Engine();
 
     // chunk_data on a host buffer; with `digests` (32 B per chunk, cap
@@ -63,6 +68,8 @@ class Engine {
 
   private:
     Engine() = default;
+    static int create_walk(cdc_algo_t algo, const uint32_t seq[4], uint32_t min, uint32_t avg, uint32_t max,
+                           int device, Engine **out);
     int init();
     int ensure_workspace(uint64_t spans, size_t n);
     int ensure_host_staging(size_t n);
@@ -70,6 +77,11 @@ class Engine {
                  uint64_t *first, hipStream_t s);
     int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                   cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
+    // Rabin / Ultra / Leap / Seq: the segment-walk engine (walk.hip).
+    bool is_walk() const { return algo_ != CDC_ALGO_FASTCDC && algo_ != CDC_ALGO_FIXED; }
+    int init_walk(const uint32_t *seq);
+    int ensure_walk_workspace(uint64_t segs, size_t n);
+    int run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64_t *first, hipStream_t s);
 
     cdc_algo_t algo_ = CDC_ALGO_FASTCDC;
     uint32_t min_ = 0, avg_ = 0, max_ = 0;
@@ -124,6 +136,16 @@ class Engine {
     uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
     uint64_t last_spans_ = 0;  // spans of the last FastCDC batch (debug_copy)
     uint64_t out_cap_ = 0;     // capacity of the current batch's output (resolve bound)
+
+    // Segment-walk engine state (Rabin / Ultra / Leap / Seq).
+    walk::WalkParams wp_{};
+    uint32_t seg_log2_ = 14;
+    uint32_t max_rounds_ = 16;     // Jacobi fix-up rounds before the serial pass
+    uint64_t *d_wtabs_ = nullptr;  // [768] rabin mod/out + leap hash tables
+    void *wws_ = nullptr;          // walk workspace arena (grow-only)
+    uint64_t wws_segs_ = 0;
+    size_t wws_streams_ = 0;
+    walk::WalkState wst_{};
 };
 
 void set_error(const std::string &msg);

@@ -1,0 +1,59 @@
+// walk.hpp -- the segment-walk engine for Rabin / UltraCDC / LeapCDC / SeqCDC
+// (reference src/chunkers/{rabin,ultra,leap,seq}.rs; DESIGN.md "Segment walk").
+//
+// Every stream of the batch is cut into segments of 2^seg_log2 bytes (>= max,
+// so no chunk spans a whole segment).  One lane owns one segment and runs the
+// algorithm's exact byte-serial cut rule (the same rule as oracle/cdc_oracle.c)
+// from a warm-up start `warm` bytes before the segment, recording the chunk
+// starts that fall inside it.  A chain from the warm-up start usually merges
+// with the true chain before the segment starts; the fix-up rounds re-walk
+// every segment whose entry differs from its predecessor's exit (Jacobi), and
+// a serial pass finishes whatever is left, so the result is exact whether or
+// not the chains merge.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cdc_kernels.hpp"
+
+namespace cdc {
+namespace walk {
+
+struct WalkParams {
+    uint32_t algo;            // cdc_algo_t: 2 rabin, 4 ultra, 5 leap, 6 seq
+    uint32_t min, avg, max;
+    uint64_t rabin_mask;      // (1 << round(log2 avg)) - 1
+    uint32_t rabin_shift;     // deg(poly) - 8
+    uint32_t leap_thr;        // eligibility threshold (CDC_LEAP_THRESHOLD)
+    uint32_t seq_mode, seq_len, seq_trig, seq_jump;
+    uint32_t cap;             // chunk starts recorded per segment
+    uint64_t warm;            // warm-up bytes before a segment
+    const uint64_t *tabs;     // device [768]: rabin mod[256], rabin out[256], leap hash[256]
+};
+
+struct WalkState {
+    uint64_t *E;      // [S] entry: first chunk start >= segment start
+    uint64_t *X;      // [S] exit: first chunk start >= segment end (or the stream length)
+    uint32_t *N;      // [S] chunk starts inside the segment
+    uint64_t *list;   // [S * cap] those starts (stream offsets)
+    uint64_t *Xs;     // [S] exits snapshot of a fix-up round
+    uint64_t *P;      // [S + 1] exclusive prefix of N (chunk index of each segment)
+    uint64_t *bsum;   // [blocks + 1] per-block sums of the prefix
+    uint64_t *first;  // [n + 1] chunk index of each stream's first chunk
+    unsigned long long *flags;  // [4]: 0 segments re-walked this round, 1 errors, 2 lowest re-walked segment
+};
+
+constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
+
+hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
+// One Jacobi round: snapshot X, then re-walk every segment whose entry is not
+// its predecessor's exit.  flags[0] counts them (the host reads it).
+hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
+// Exact in-order pass over all segments from the lowest one re-walked.
+hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
+// Prefix of N, first[], and the Chunk{offset,length} output.
+hipError_t launch_emit(const StreamTable &st, const WalkParams &wp, const WalkState &ws, void *d_out,
+                       uint64_t out_cap, hipStream_t s);
+
+}  // namespace walk
+}  // namespace cdc

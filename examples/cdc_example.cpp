@@ -51,6 +51,26 @@ int main() {
         for (size_t i = 0; i < spans.size(); ++i)
             if (spans[i] != chunks[i].length()) return 5;  // segmentation invariance
         std::printf("write path: %zu spans == whole-buffer chunks; chunk_data time %.3f s\n", spans.size(), chunk_s);
+
+        // The other chunker families (segment-walk engine): tiling + the
+        // same segmentation invariance through the write path.
+        const SizeParams sz{4 * KB, 8 * KB, 16 * KB};
+        std::vector<std::unique_ptr<Chunker>> others;
+        others.emplace_back(new RabinChunker(sz));
+        others.emplace_back(new UltraChunker(sz));
+        others.emplace_back(new LeapChunker(sz));
+        others.emplace_back(new SeqChunker(OperationMode::Increasing, sz));
+        for (auto &ch : others) {
+            const auto oc = ch->chunk_data(data);
+            size_t tot = 0;
+            for (const auto &c : oc) tot += c.length();
+            if (tot != n || oc.front().offset() != 0) return 6;
+            const auto os = ch->write_spans(data.data(), n);
+            if (os.size() != oc.size()) return 7;
+            for (size_t i = 0; i < os.size(); ++i)
+                if (os[i] != oc[i].length()) return 8;
+            std::printf("%s: %zu chunks, write path identical\n", ch->debug().c_str(), oc.size());
+        }
     } catch (const Error &e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

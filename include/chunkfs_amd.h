@@ -37,11 +37,11 @@ typedef struct cdc_chunk {
 typedef enum cdc_algo {
     CDC_ALGO_FASTCDC = 0, /* FastChunker  (src/chunkers/fast.rs)        */
     CDC_ALGO_FIXED = 1,   /* FSChunker    (src/chunkers/fixed_size.rs)  */
-    CDC_ALGO_RABIN = 2,   /* RabinChunker -- CDC_ENOTSUP (no oracle: cdc-chunkers 0.1.3 absent) */
-    CDC_ALGO_SUPER = 3,   /* SuperChunker -- CDC_ENOTSUP */
-    CDC_ALGO_ULTRA = 4,   /* UltraChunker -- CDC_ENOTSUP */
-    CDC_ALGO_LEAP = 5,    /* LeapChunker  -- CDC_ENOTSUP */
-    CDC_ALGO_SEQ = 6      /* SeqChunker   -- CDC_ENOTSUP */
+    CDC_ALGO_RABIN = 2,   /* RabinChunker (src/chunkers/rabin.rs)    -- parity unpinned */
+    CDC_ALGO_SUPER = 3,   /* SuperChunker (src/chunkers/supercdc.rs) -- CDC_ENOTSUP */
+    CDC_ALGO_ULTRA = 4,   /* UltraChunker (src/chunkers/ultra.rs)    -- parity unpinned */
+    CDC_ALGO_LEAP = 5,    /* LeapChunker  (src/chunkers/leap.rs)     -- parity unpinned */
+    CDC_ALGO_SEQ = 6      /* SeqChunker   (src/chunkers/seq.rs)      -- parity unpinned */
 } cdc_algo_t;
 
 #define CDC_OK 0
@@ -56,9 +56,26 @@ typedef struct cdc_handle cdc_handle_t;
  *   CDC_ALGO_FASTCDC: FastChunker::new(SizeParams{min,avg,max}) (fast.rs:11-15);
  *                     v2020 FastCDC, Level1 normalization (fast.rs:37).
  *   CDC_ALGO_FIXED:   FSChunker::new(min) (fixed_size.rs:19-23); avg/max ignored.
+ *   CDC_ALGO_RABIN / _ULTRA / _LEAP: RabinChunker / UltraChunker / LeapChunker
+ *                     ::new(SizeParams{min,avg,max}) (rabin.rs:13-20,
+ *                     ultra.rs:12-16, leap.rs:12-16).  The reference's crate
+ *                     (cdc-chunkers 0.1.3) is absent: the cut rules restate the
+ *                     published algorithms, parity unpinned.
+ *                     Sizes: 0 < min <= avg <= max; Ultra min >= 8, Leap min >= 32.
+ *   CDC_ALGO_SEQ:     SeqChunker with OperationMode::Increasing and the default
+ *                     Config (cdc_create_seq for the full constructor).
+ *   CDC_ALGO_SUPER:   CDC_ENOTSUP.
  * Returns CDC_OK and *out, or a negative code. */
 int cdc_create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
                int device, cdc_handle_t **out);
+
+/* SeqChunker::new(mode, sizes, config) (seq.rs:16-24): mode 0 = Increasing,
+ * 1 = Decreasing; config = seq_length (pairs in the mode's direction that
+ * end a chunk), jump_trigger (opposing pairs before a jump), jump_size
+ * (bytes skipped); defaults 5 / 50 / 256 (include/chunkfs_amd_cdc_params.h). */
+int cdc_create_seq(uint32_t mode, uint32_t seq_length, uint32_t jump_trigger,
+                   uint32_t jump_size, uint32_t min, uint32_t avg, uint32_t max,
+                   int device, cdc_handle_t **out);
 
 /* Drop(Chunker). */
 void cdc_destroy(cdc_handle_t *h);
@@ -73,8 +90,9 @@ int64_t cdc_chunk_data(cdc_handle_t *h, const uint8_t *data, size_t len,
                        cdc_chunk_t *out, size_t cap);
 
 /* Chunker::estimate_chunk_count (src/lib.rs:85): the reference's own formula,
- * len/min for FastCDC (fast.rs:47-49), len/size + 1 for fixed
- * (fixed_size.rs:45-47). */
+ * len/min for FastCDC (fast.rs:47-49), Rabin, Ultra, Leap (rabin.rs:53-55,
+ * ultra.rs:41-43, leap.rs:41-43), len/avg for Seq (seq.rs:52-54), len/size + 1
+ * for fixed (fixed_size.rs:45-47). */
 size_t cdc_estimate_chunk_count(const cdc_handle_t *h, size_t len);
 
 /* A strict upper bound on the chunk count of `len` bytes (len/min + 1). */

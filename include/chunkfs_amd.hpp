@@ -7,6 +7,7 @@
 //   SizeParams {min, avg, max}      chunkers/mod.rs chunkfs_amd::SizeParams
 //   FastChunker                     chunkers/fast.rs        chunkfs_amd::FastChunker
 //   FSChunker                       chunkers/fixed_size.rs  chunkfs_amd::FSChunker
+//   Rabin/Ultra/Leap/SeqChunker     chunkers/{rabin,ultra,leap,seq}.rs  same names
 //   ChunkStorage::write spans       system/storage.rs:78-103  Chunker::write_spans
 //
 // The reference panics on invalid sizes; here constructors throw
@@ -100,6 +101,7 @@ class Chunker {
     cdc_handle_t *handle() { return h_; }
 
   protected:
+    Chunker() = default;
     Chunker(cdc_algo_t algo, size_t min, size_t avg, size_t max, int device) {
         check(cdc_create(algo, (uint32_t)min, (uint32_t)avg, (uint32_t)max, device, &h_));
     }
@@ -126,6 +128,42 @@ class FSChunker : public Chunker {
 
   private:
     size_t chunk_size_;
+};
+
+// RabinChunker / UltraChunker / LeapChunker (src/chunkers/{rabin,ultra,leap}.rs):
+// published algorithms, parity unpinned (cdc-chunkers 0.1.3 absent); sizes are
+// explicit because the crate's SizeParams::*_default() values are unknown.
+class RabinChunker : public Chunker {
+  public:
+    explicit RabinChunker(SizeParams sizes, int device = 0)
+        : Chunker(CDC_ALGO_RABIN, sizes.min, sizes.avg, sizes.max, device) {}
+};
+
+class UltraChunker : public Chunker {
+  public:
+    explicit UltraChunker(SizeParams sizes, int device = 0)
+        : Chunker(CDC_ALGO_ULTRA, sizes.min, sizes.avg, sizes.max, device) {}
+};
+
+class LeapChunker : public Chunker {
+  public:
+    explicit LeapChunker(SizeParams sizes, int device = 0)
+        : Chunker(CDC_ALGO_LEAP, sizes.min, sizes.avg, sizes.max, device) {}
+};
+
+// seq::OperationMode and seq::Config (re-exported at src/chunkers/seq.rs:3).
+enum class OperationMode : uint32_t { Increasing = 0, Decreasing = 1 };
+struct SeqConfig {
+    uint32_t seq_length = 5, jump_trigger = 50, jump_size = 256;
+};
+
+// SeqChunker::new(mode, sizes, config) (src/chunkers/seq.rs:16-24).
+class SeqChunker : public Chunker {
+  public:
+    SeqChunker(OperationMode mode, SizeParams sizes, SeqConfig config = {}, int device = 0) : Chunker() {
+        check(cdc_create_seq((uint32_t)mode, config.seq_length, config.jump_trigger, config.jump_size,
+                             (uint32_t)sizes.min, (uint32_t)sizes.avg, (uint32_t)sizes.max, device, &h_));
+    }
 };
 
 // ChunkerRef (src/lib.rs:89): shared handle to one chunker.

@@ -51,6 +51,19 @@ def lib():
         L.oracle_time_fastcdc.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int64)]
         L.oracle_time_fastcdc.restype = ctypes.c_double
+        L.oracle_cdc_chunk.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                       ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, u64p, u64p,
+                                       ctypes.c_uint64]
+        L.oracle_cdc_chunk.restype = ctypes.c_int64
+        L.oracle_cdc_check.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_cdc_check.restype = ctypes.c_int
+        L.oracle_leap_threshold.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_leap_threshold.restype = ctypes.c_uint32
+        L.oracle_cdc_tables.argtypes = [u64p, u64p, u64p]
+        L.oracle_cdc_tables.restype = None
+        L.oracle_time_cdc.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int64)]
+        L.oracle_time_cdc.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -101,6 +114,36 @@ def fixed(n, cs):
     return np.stack([off[:cnt], ln[:cnt]], axis=1)
 
 
+# cdc_algo_t numbering (include/chunkfs_amd.h).
+ALGOS = {"fast": 0, "fixed": 1, "rabin": 2, "ultra": 4, "leap": 5, "seq": 6}
+
+
+def cdc(algo, data, mn, avg, mx, seqcfg=None):
+    """(n, 2) uint64 (offset, length) of Rabin / Ultra / Leap / Seq over the whole
+    buffer (oracle/cdc_oracle.c; parity unpinned, see the header there).
+    seqcfg = (mode, seq_length, jump_trigger, jump_size) for "seq"."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    n = data.size
+    cap = n // mn + 2
+    off = np.empty(cap, dtype=np.uint64)
+    ln = np.empty(cap, dtype=np.uint64)
+    cfg = None if seqcfg is None else np.ascontiguousarray(seqcfg, dtype=np.uint32)
+    cnt = lib().oracle_cdc_chunk(ALGOS[algo], _ptr(data), n, mn, avg, mx,
+                                 None if cfg is None else _ptr(cfg), _u64p(off), _u64p(ln), cap)
+    if cnt < 0:
+        raise ValueError("invalid sizes")
+    assert cnt <= cap
+    return np.stack([off[:cnt], ln[:cnt]], axis=1)
+
+
+def time_cdc(algo, data, mn, avg, mx):
+    """Single-thread wall seconds of one whole-buffer pass (cpu_baseline)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    cnt = ctypes.c_int64(0)
+    t = lib().oracle_time_cdc(ALGOS[algo], _ptr(data), data.size, mn, avg, mx, ctypes.byref(cnt))
+    return t, cnt.value
+
+
 def fs_write(algo, data, mn, avg=0, mx=0, seg_size=1 << 20, gear=None):
     """StorageWriter mirror: span lengths of one write call, and summed chunk_data seconds."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
@@ -108,7 +151,7 @@ def fs_write(algo, data, mn, avg=0, mx=0, seg_size=1 << 20, gear=None):
     out = np.empty(cap, dtype=np.uint64)
     secs = ctypes.c_double(0.0)
     g = None if gear is None else np.ascontiguousarray(gear, dtype=np.uint64)
-    cnt = lib().oracle_fs_write(0 if algo == "fast" else 1, _ptr(data), data.size, mn, avg, mx,
+    cnt = lib().oracle_fs_write(ALGOS[algo], _ptr(data), data.size, mn, avg, mx,
                                 None if g is None else _ptr(g), seg_size, _u64p(out), cap,
                                 ctypes.byref(secs))
     if cnt < 0:
@@ -197,6 +240,153 @@ def py_fastcdc(data, mn, avg, mx, gear=None):
                 if h & (ms if p < ce else ml) == 0:
                     cut = p
                     break
+        out.append((pos, cut))
+        pos += cut
+    return np.array(out, dtype=np.uint64).reshape(-1, 2)
+
+
+# ---------------------------------------------------------------------------
+# Pure-Python twins of the Rabin / Ultra / Leap / Seq restatements (small
+# inputs only).  Different code shapes from the C oracle: Rabin by direct
+# GF(2) polynomial arithmetic (no tables), Ultra with the 8-byte distance
+# recomputed at every tested position (C keeps it incrementally).
+
+def _cdc_params():
+    path = os.path.join(ROOT, "include", "chunkfs_amd_cdc_params.h")
+    txt = open(path).read()
+    import re
+    d = {}
+    for k, v in re.findall(r"#define (CDC_[A-Z_]+) (0x[0-9A-Fa-f]+|[0-9]+)", txt):
+        d[k] = int(v, 0)
+    body = txt.split("CDC_LEAP_THRESHOLD[33]", 1)[1].split("{", 1)[1].split("}", 1)[0]
+    d["THR"] = [int(x, 16) for x in re.findall(r"0x([0-9A-Fa-f]+)u", body)]
+    return d
+
+
+def _log2_round(x):
+    b = x.bit_length() - 1
+    if 0 < b < 63 and x - (1 << b) >= (1 << b) // 2:
+        b += 1
+    return b
+
+
+def _polmod(x, p):
+    dp = p.bit_length() - 1
+    while x and x.bit_length() - 1 >= dp:
+        x ^= p << (x.bit_length() - 1 - dp)
+    return x
+
+
+def _mix64(z):
+    M = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
+def _py_cut(algo, d, s, n, mn, avg, mx, P, cfg):
+    if n <= mn:
+        return n
+    end = min(n, mx)
+    if algo == "rabin":
+        W, poly = P["CDC_RABIN_WINDOW"], P["CDC_RABIN_POLY"]
+        xw = _polmod(1 << (8 * W), poly)  # x^(8W) mod P
+        mask = (1 << _log2_round(avg)) - 1
+        start = mn - W if mn >= W else 0
+        h = 0
+        for i in range(start, end):
+            o = d[s + i - W] if i >= start + W else 0
+            h = (h << 8) ^ d[s + i]
+            # subtract o * x^(8W): multiply o by xw in GF(2)
+            t = 0
+            for bit in range(8):
+                if (o >> bit) & 1:
+                    t ^= xw << bit
+            h = _polmod(h ^ t, poly)
+            if i + 1 >= mn and (h & mask) == 0:
+                return i + 1
+        return end
+    if algo == "ultra":
+        pat = P["CDC_ULTRA_PATTERN"]
+        normal = avg
+        end = n
+        if n >= mx:
+            end = mx
+        elif n <= normal:
+            normal = n
+        lec = 0
+        i = mn
+        while i + 8 <= end:
+            blk_in, blk_out = d[s + i:s + i + 8], d[s + i - 8:s + i]
+            if blk_in == blk_out:
+                lec += 1
+                if lec >= P["CDC_ULTRA_LEST"]:
+                    return i + 8
+                i += 8
+                continue
+            lec = 0
+            mask = P["CDC_ULTRA_MASK_L"] if i >= normal else P["CDC_ULTRA_MASK_S"]
+            for j in range(8):
+                q = s + i + j
+                dist = sum(bin(b ^ pat).count("1") for b in d[q - 8:q])
+                if dist & mask == 0:
+                    return i + j
+            i += 8
+        return end
+    if algo == "leap":
+        M = (1 << 64) - 1
+        E = [_mix64((P["CDC_LEAP_SEED"] + (b + 1) * 0x9E3779B97F4A7C15) & M) for b in range(256)]
+        thr = P["THR"][min(_log2_round(max(avg - mn, 1)), 32)]
+
+        def h(p):
+            v = 0
+            for j in range(P["CDC_LEAP_WSIZE"]):
+                e, r = E[d[s + p - j]], (11 * j) % 64
+                v = (v + (((e << r) | (e >> (64 - r))) & M if r else e)) & M
+            return v
+        c = mn
+        while c <= end:
+            k = 0
+            while k < P["CDC_LEAP_WINDOWS"]:
+                v = h(c - 1 - k)
+                v = v >> 32 if k < P["CDC_LEAP_PRIMARY"] else v & 0xFFFFFFFF
+                if v >= thr:
+                    break
+                k += 1
+            if k == P["CDC_LEAP_WINDOWS"]:
+                return c
+            c += P["CDC_LEAP_WINDOWS"] - k
+        return end
+    if algo == "seq":
+        mode, length, trig, jump = cfg
+        cnt = opp = 0
+        i = mn
+        while i < end:
+            a, b = d[s + i - 1], d[s + i]
+            if (b < a) if mode else (b > a):
+                cnt += 1
+                if cnt >= length:
+                    return i + 1
+            else:
+                cnt = 0
+                opp += 1
+                if opp >= trig:
+                    opp = 0
+                    i += jump
+                    continue
+            i += 1
+        return end
+    raise ValueError(algo)
+
+
+def py_cdc(algo, data, mn, avg, mx, seqcfg=None):
+    P = _cdc_params()
+    cfg = tuple(seqcfg) if seqcfg is not None else (0, P["CDC_SEQ_LENGTH"], P["CDC_SEQ_JUMP_TRIGGER"],
+                                                     P["CDC_SEQ_JUMP_SIZE"])
+    d = bytes(bytearray(np.asarray(data, dtype=np.uint8)))
+    out, pos = [], 0
+    while pos < len(d):
+        cut = _py_cut(algo, d, pos, len(d) - pos, mn, avg, mx, P, cfg)
         out.append((pos, cut))
         pos += cut
     return np.array(out, dtype=np.uint64).reshape(-1, 2)

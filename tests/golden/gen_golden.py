@@ -77,7 +77,55 @@ CASES = [
 ]
 
 
+# Rabin / UltraCDC / LeapCDC / SeqCDC vectors (cdc_walk_selfconsistent.json):
+# oracle/cdc_oracle.c cross-checked by oracle.py:py_cdc.  LABEL: "self-consistent,
+# unverified vs cdc-chunkers 0.1.3" (the crate is absent offline).
+WALK_CASES = [
+    # (algo, pattern, len, seed, min, avg, max)
+    ("rabin", "splitmix64", 0, 1, 2048, 4096, 8192),
+    ("rabin", "splitmix64", 2047, 1, 2048, 4096, 8192),
+    ("rabin", "splitmix64", 300001, 2, 2048, 4096, 8192),
+    ("rabin", "splitmix64", 200000, 3, 64, 256, 1024),
+    ("rabin", "const", 100000, 0, 512, 1024, 4096),
+    ("rabin", "lowentropy", 200000, 4, 512, 2048, 8192),
+    ("ultra", "splitmix64", 300000, 5, 4096, 8192, 16384),
+    ("ultra", "splitmix64", 200003, 6, 1024, 2048, 8192),
+    ("ultra", "const", 100000, 7, 1024, 2048, 8192),
+    ("ultra", "periodic", 200000, 61, 2048, 4096, 16384),
+    ("leap", "splitmix64", 300000, 8, 4096, 8192, 16384),
+    ("leap", "splitmix64", 150001, 9, 256, 1024, 4096),
+    ("leap", "lowentropy", 150000, 10, 512, 2048, 8192),
+    ("seq", "splitmix64", 300000, 11, 4096, 8192, 16384),
+    ("seq", "splitmix64", 100001, 12, 64, 256, 1024),
+    ("seq", "const", 50000, 13, 1000, 2000, 5000),
+    ("seq", "periodic", 200000, 4096, 2048, 4096, 16384),
+]
+
+
+def gen_walk():
+    vecs = []
+    for algo, pattern, n, seed, mn, avg, mx in WALK_CASES:
+        data = make_input(pattern, n, seed)
+        c = oracle.cdc(algo, data, mn, avg, mx)
+        p = oracle.py_cdc(algo, data, mn, avg, mx)
+        assert p.shape == c.shape and (p == c).all(), ("C and Python oracles disagree", algo, pattern, n)
+        vecs.append({
+            "algo": algo, "pattern": pattern, "len": n, "seed": seed, "min": mn, "avg": avg, "max": mx,
+            "input_sha256": hashlib.sha256(data.tobytes()).hexdigest(),
+            "lengths": [int(x) for x in c[:, 1]],
+        })
+    meta = {
+        "label": "self-consistent, unverified vs cdc-chunkers 0.1.3 (crate absent offline)",
+        "generator": "tests/golden/gen_golden.py via oracle/cdc_oracle.c, cross-checked by oracle.py:py_cdc",
+        "vectors": vecs,
+    }
+    with open(os.path.join(HERE, "cdc_walk_selfconsistent.json"), "w") as f:
+        json.dump(meta, f, separators=(",", ":"))
+    return len(vecs)
+
+
 def main():
+    print("wrote", gen_walk(), "Rabin/Ultra/Leap/Seq vectors")
     vecs = []
     for pattern, n, seed, mn, avg, mx in CASES:
         data = make_input(pattern, n, seed)

@@ -81,10 +81,30 @@ def test_invalid_sizes_rejected_before_device():
 
 def test_unsupported_algorithms_raise():
     import chunkfs_amd
-    for cls in (chunkfs_amd.RabinChunker, chunkfs_amd.SuperChunker, chunkfs_amd.UltraChunker,
-                chunkfs_amd.LeapChunker, chunkfs_amd.SeqChunker):
-        with pytest.raises(NotImplementedError):
+    with pytest.raises(NotImplementedError):
+        chunkfs_amd.SuperChunker()
+
+
+def test_walk_chunkers_need_explicit_sizes():
+    import chunkfs_amd as c
+    for cls in (c.RabinChunker, c.UltraChunker, c.LeapChunker):
+        with pytest.raises(TypeError):
             cls()
+    with pytest.raises(TypeError):
+        c.SeqChunker(c.OperationMode.Increasing)
+
+
+def test_walk_chunkers_reject_bad_sizes_before_device():
+    import chunkfs_amd as c
+    bad = [(c.RabinChunker, (0, 10, 20)), (c.UltraChunker, (4, 8, 16)), (c.LeapChunker, (16, 64, 128)),
+           (c.RabinChunker, (100, 50, 200))]
+    for cls, s in bad:
+        with pytest.raises(c.CdcError) as ei:
+            cls(c.SizeParams(*s))
+        assert ei.value.code == -1
+    with pytest.raises(c.CdcError) as ei:
+        c.SeqChunker(c.OperationMode.Decreasing, c.SizeParams(64, 128, 256), c.SeqConfig(0, 50, 256))
+    assert ei.value.code == -1
 
 
 def test_python_mirror_debug_strings():
