@@ -5,7 +5,7 @@ TAG=${1:-exp}
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
-for D in 0 256 512 128 0; do
+for D in ${DIAGS:-0 256 512 128 0}; do
     echo "== DIAG=$D" >> $OUT/exp_$TAG.log
     timeout -k 10 120 python -u tools/diag_resolve.py $D >> $OUT/exp_$TAG.log 2>&1
     rc=$?; echo "DIAG=$D rc=$rc"
