@@ -331,6 +331,143 @@ def algo_lines(args, eng, steps):
     return res
 
 
+def config5_lines(args, eng, nbytes=256 << 20, steps=2):
+    """Config 5's size sweep (BASELINE.json configs[4]) on one GPU: UltraCDC and
+    LeapCDC (plus Rabin and Seq) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg
+    (SURVEY.md §8d), over a 256 MiB prefix of the bench stream; device GiB/s,
+    fraction of HBM peak, bit-exactness vs the oracle.  SuperCDC is not
+    implemented (CDC_ENOTSUP)."""
+    import numpy as np
+    import torch
+    import chunkfs_amd as cfa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n = min(nbytes, eng.lens[0])
+    buf = eng.bufs[0]
+    host = buf[:n].cpu().numpy() if not args.no_parity else None
+    res = {}
+    for avg in (2048, 8192, 65536):
+        sz = cfa.SizeParams(avg // 4, avg, avg * 8)
+        for name in ("ultra", "leap", "rabin", "seq"):
+            cls = {"rabin": cfa.RabinChunker, "ultra": cfa.UltraChunker, "leap": cfa.LeapChunker}.get(name)
+            ch = cls(sz, device=eng.local) if cls else cfa.SeqChunker(0, sz, device=eng.local)
+            cap = ch.batch_max_chunks([n])
+            out = torch.empty((cap, 2), dtype=torch.int64, device=eng.dev)
+            first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+            torch.cuda.synchronize()
+            el = (time.perf_counter() - t0) / steps
+            line = {"sizes": [sz.min, sz.avg, sz.max], "GiBps": n / el / (1 << 30),
+                    "frac_of_hbm": n / el / 1e9 / HBM_PEAK_GBS, "chunks": int(first[1]),
+                    "rewalked_segments": ch.last_timing()["fixup_iterations"]}
+            if host is not None:
+                got = out[:int(first[1])].cpu().numpy().view(np.uint64)
+                ref = oracle.cdc(name, host, sz.min, sz.avg, sz.max)
+                line["parity_vs_oracle"] = bool(got.shape == ref.shape and (got == ref).all())
+            res[f"{name}_avg{avg // 1024}k"] = line
+            ch.close()
+            del out
+    return {"bytes": int(n), "lines": res}
+
+
+def versioned_archive(base_bytes, versions, seed=3):
+    """SURVEY.md §8d config 3's offline substitute for the gcc tarball: a seeded
+    random base blob and `versions - 1` successive copies, each with seeded
+    overwrites, inserts and deletes totalling ~1 % of its bytes."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    rng = np.random.default_rng(seed)
+    out = [oracle.splitmix64_bytes(base_bytes, seed)]
+    for _ in range(versions - 1):
+        v = out[-1]
+        budget = v.size // 100
+        parts, pos = [], 0
+        for p in np.sort(rng.choice(v.size - 8192, size=max(1, budget // 2048), replace=False)):
+            if p < pos:
+                continue
+            parts.append(v[pos:p])
+            k = int(rng.integers(64, 4096))
+            op = int(rng.integers(0, 3))
+            if op == 0:    # overwrite k bytes
+                parts.append(rng.integers(0, 256, k, dtype=np.uint8))
+                pos = p + k
+            elif op == 1:  # insert k bytes
+                parts.append(rng.integers(0, 256, k, dtype=np.uint8))
+                pos = p
+            else:          # delete k bytes
+                pos = p + k
+        parts.append(v[pos:])
+        out.append(np.ascontiguousarray(np.concatenate(parts)))
+    return out
+
+
+def config3_line(args, local, base_bytes=64 << 20, versions=8):
+    """Config 3 (BASELINE.json configs[2]): RabinChunker 2/4/8 KiB over a
+    versioned archive; every version is one file write (a fresh StorageWriter,
+    storage.rs:79).  GPU: chunk -> SHA-256 per chunk -> dedup index, all
+    device-resident; dedup ratio = size_written / unique bytes (storage.rs:
+    203-205).  CPU: the oracle's chunks, hashlib SHA-256 and a dict (first
+    insert wins, database.rs:76), single thread."""
+    import hashlib
+    import numpy as np
+    import torch
+    import chunkfs_amd as cfa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    sizes = (2048, 4096, 8192)
+    files = versioned_archive(base_bytes, versions)
+    total = sum(f.size for f in files)
+    dev = torch.device("cuda", local)
+    bufs = [torch.from_numpy(f).to(dev) for f in files]
+    ch = cfa.RabinChunker(cfa.SizeParams(*sizes), device=local)
+    lens = [f.size for f in files]
+    cap = ch.batch_max_chunks(lens)
+    out = torch.empty((cap, 2), dtype=torch.int64, device=dev)
+    dig = torch.empty((cap, 32), dtype=torch.uint8, device=dev)
+
+    def gpu_pass():
+        first = ch.chunk_batch_device([b.data_ptr() for b in bufs], lens, out.data_ptr(), cap)
+        ix = cfa.DedupIndex(int(first[-1]) + 64, device=local)
+        for i, b in enumerate(bufs):
+            a, z = int(first[i]), int(first[i + 1])
+            ch.sha256_chunks_device(b.data_ptr(), out[a:].data_ptr(), z - a, dig[a:].data_ptr())
+            ix.insert_device(dig[a:].data_ptr(), out[a:].data_ptr(), z - a)
+        torch.cuda.synchronize()
+        return first, ix.stats()
+
+    gpu_pass()
+    t0 = time.perf_counter()
+    first, st = gpu_pass()
+    t_gpu = time.perf_counter() - t0
+    got = out[:int(first[-1])].cpu().numpy().view(np.uint64)
+    t0 = time.perf_counter()
+    db, written, parity = {}, 0, True
+    for i, f in enumerate(files):
+        ref = oracle.cdc("rabin", f, *sizes)
+        parity &= bool(np.array_equal(got[int(first[i]):int(first[i + 1])], ref))
+        for o, ln in ref:
+            d = hashlib.sha256(f[int(o):int(o) + int(ln)].tobytes()).digest()
+            db.setdefault(d, int(ln))
+            written += int(ln)
+    t_cpu = time.perf_counter() - t0
+    cpu_ratio = written / sum(db.values())
+    ch.close()
+    return {"workload": f"config3 substitute: {versions} versions of a {base_bytes} B splitmix64 base, "
+                        "~1 % seeded overwrites/inserts/deletes per version (gcc tarball unavailable offline)",
+            "algo": "RabinCDC (parity unpinned)", "sizes": list(sizes), "bytes": int(total),
+            "chunks": int(first[-1]), "gpu_dedup_ratio": st["cdc_dedup_ratio"], "cpu_dedup_ratio": cpu_ratio,
+            "dedup_ratio_equal": bool(abs(st["cdc_dedup_ratio"] - cpu_ratio) < 1e-12),
+            "chunks_bit_exact": parity, "unique_chunks": st["unique_chunks"],
+            "gpu_GiBps": total / t_gpu / (1 << 30),
+            "gpu_definition": "device-resident: Rabin chunking + SHA-256 per chunk + dedup index inserts, wall time",
+            "cpu_GiBps": total / t_cpu / (1 << 30),
+            "cpu_definition": "oracle Rabin (C) + hashlib SHA-256 + dict, single thread"}
+
+
 def host_path_leg(eng):
     """PCIe-inclusive rates of the host boundary, recorded beside `value`,
     never as it: cdc_chunk_data on a 1 GiB host buffer, and the
@@ -452,6 +589,8 @@ def main(argv=None):
             extras["sweep"] = sweep_lines(args, eng, max(5, args.steps // 2))
         if not args.no_algos and args.workload == "stream":
             extras["other_chunkers"] = algo_lines(args, eng, 3)
+            extras["config3"] = config3_line(args, local)
+            extras["config5_1gpu"] = config5_lines(args, eng)
         if args.cpu_seconds > 0:
             extras["cpu_baseline"] = cpu_baseline_leg(args, eng.bufs[0][:shard.lens[0]].cpu().numpy())
             fw = extras.get("host_path", {}).get("fs_write_1MiB_segments")

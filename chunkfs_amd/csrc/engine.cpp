@@ -659,13 +659,13 @@ int Engine::init_walk(const uint32_t *seq) {
     wp.seq_trig = seq[2];
     wp.seq_jump = seq[3];
     // Segments of 2^seg_log2 bytes (one lane each) and a warm-up of `warm`
-    // bytes; CHUNKFS_AMD_WALK="seg_log2,warm_over_max" overrides (experiments).
+    // bytes; CHUNKFS_AMD_WALK="seg_log2,warm_over_avg" overrides (experiments).
     // Defaults (tools/walk_bench.py sweeps on MI355X): segments of
-    // >= 2 max and >= 32 KiB, a warm-up of 4 max (a chain from an arbitrary
-    // start merges with the true one within a few chunks).
-    const uint32_t l2 = ceil_log2(max_) + 1;
+    // >= 4 avg and >= 32 KiB, a warm-up of 8 avg (a chain from an arbitrary
+    // start merges with the true one within a few content-defined cuts).
+    const uint32_t l2 = ceil_log2(avg_) + 2;
     seg_log2_ = l2 < 15 ? 15 : l2;
-    uint64_t warm_mult = 4;
+    uint64_t warm_mult = 8;
     if (const char *w = std::getenv("CHUNKFS_AMD_WALK")) {
         unsigned a = 0, b = 0;
         if (std::sscanf(w, "%u,%u", &a, &b) == 2 && a >= 10 && a <= 30) {
@@ -673,8 +673,17 @@ int Engine::init_walk(const uint32_t *seq) {
             warm_mult = b;
         }
     }
-    wp.warm = warm_mult * max_;
+    wp.warm = warm_mult * avg_;
     wp.cap = (uint32_t)((1ull << seg_log2_) / min_ + 2);
+    // Bitmap mode for the windowed rules: Rabin when every tested
+    // digest is a full window (min >= 48), UltraCDC, LeapCDC.
+    // CHUNKFS_AMD_WALK_BYTES=1 forces the byte walks (A/B experiments).
+    wp.nbm = algo_ == CDC_ALGO_RABIN ? (min_ >= CDC_RABIN_WINDOW ? 1u : 0u)
+           : algo_ == CDC_ALGO_ULTRA ? 3u : algo_ == CDC_ALGO_LEAP ? 2u : 0u;
+    if (const char *b = std::getenv("CHUNKFS_AMD_WALK_BYTES"))
+        if (std::atoi(b) != 0) wp.nbm = 0;
+    wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);
+    wp.bm = nullptr;
     // Tables: Rabin mod/out (appending a byte; sliding one out of the window),
     // LeapCDC window-hash table.
     uint64_t t[768];
@@ -708,6 +717,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     const size_t oE = take(S * 8), oX = take(S * 8), oXs = take(S * 8), oP = take((S + 1) * 8);
     const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
     const size_t oF = take((N + 1) * 8), oG = take(4 * 8);
+    const size_t oBM = take(S * (size_t)wp_.seg_words * wp_.nbm * 8);  // predicate bitmaps
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(wws_);
     wws_ = nullptr;
@@ -727,6 +737,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wst_.bsum = reinterpret_cast<uint64_t *>(b + oB);
     wst_.first = reinterpret_cast<uint64_t *>(b + oF);
     wst_.flags = reinterpret_cast<unsigned long long *>(b + oG);
+    wp_.bm = wp_.nbm ? reinterpret_cast<uint64_t *>(b + oBM) : nullptr;
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
@@ -739,6 +750,7 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     uint64_t *h_first = h_flags + 4;
     HIP_TRY(hipMemsetAsync(wst_.flags, 0, 4 * 8, s));
     HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(walk::launch_bits(st, wp_, s));
     HIP_TRY(walk::launch_walk(st, wp_, wst_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
     // Jacobi rounds: re-walk every segment whose entry is not its predecessor's

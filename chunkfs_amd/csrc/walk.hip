@@ -94,6 +94,26 @@ struct Reader {
         ensure(p, p);
         return raw(p);
     }
+    // Bitmap mode: word widx (8-byte aligned in the stream's bitmap bytes).
+    __device__ __forceinline__ uint64_t word(uint64_t widx) {
+        ensure(widx * 8, widx * 8 + 7);
+        return *reinterpret_cast<const uint64_t *>(slot + (widx * 8 - w0));
+    }
+    // n (1..64) bits of bitmap b from position p, bit j = position p + j.
+    __device__ __forceinline__ uint64_t bits(uint32_t nbm, uint32_t b, uint64_t p, uint32_t n) {
+        const uint64_t k = p >> 6;
+        const uint32_t sh = (uint32_t)(p & 63);
+        uint64_t v;
+        if (sh + n <= 64) {
+            v = word(k * nbm + b) >> sh;
+        } else {
+            ensure(k * nbm * 8, ((k + 1) * nbm + b) * 8 + 7);
+            const uint64_t lo = *reinterpret_cast<const uint64_t *>(slot + ((k * nbm + b) * 8 - w0));
+            const uint64_t hi = *reinterpret_cast<const uint64_t *>(slot + (((k + 1) * nbm + b) * 8 - w0));
+            v = (lo >> sh) | (hi << (64 - sh));
+        }
+        return n == 64 ? v : v & ((1ull << n) - 1);
+    }
     __device__ __forceinline__ uint64_t at8(uint64_t p) {
         ensure(p, p + 7);
         uint64_t v = 0;
@@ -212,17 +232,94 @@ __device__ uint64_t cut_seq(Reader &r, uint64_t s, uint64_t n, const WalkParams 
     return end;
 }
 
-template <int kAlgo>
+// ---- the same rules over the predicate bitmaps (bits_kernel) ---------------
+// Rabin (min >= 48): every tested digest is a full 48-byte window, so a hit is
+// the bitmap bit; the cut is the first hit in [s+min-1, s+end-1], plus one.
+__device__ uint64_t cut_rabin_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+    if (n <= wp.min) return n;
+    const uint64_t end = n < wp.max ? n : wp.max;
+    const uint64_t lo = s + wp.min - 1, hi = s + end - 1;
+    for (uint64_t k = lo >> 6; k <= (hi >> 6); ++k) {
+        uint64_t w = r.word(k);
+        if (k == (lo >> 6)) w &= ~0ull << (lo & 63);
+        if (k == (hi >> 6) && (hi & 63) != 63) w &= (2ull << (hi & 63)) - 1;
+        if (w) return k * 64 + (uint64_t)__builtin_ctzll(w) - s + 1;
+    }
+    return end;
+}
+
+// UltraCDC over bitmaps 0 (dist & MASK_S == 0), 1 (dist & MASK_L == 0) and
+// 2 (the 8 bytes at q repeat the 8 before).  64 positions at a time while no
+// block start repeats and no position hits, else block by block as cut_ultra.
+__device__ uint64_t cut_ultra_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+    if (n <= wp.min) return n;
+    uint64_t normal = wp.avg, end = n;
+    if (n >= wp.max) end = wp.max;
+    else if (n <= normal) normal = n;
+    uint32_t lec = 0;
+    uint64_t i = wp.min;
+    while (i + 8 <= end) {
+        if (i + 64 <= end && (i >= normal || i + 56 < normal)) {
+            const uint64_t e = r.bits(3, 2, s + i, 64) & 0x0101010101010101ull;
+            const uint64_t m = r.bits(3, i >= normal ? 1 : 0, s + i, 64);
+            if ((e | m) == 0) {
+                lec = 0;
+                i += 64;
+                continue;
+            }
+        }
+        if (r.bits(3, 2, s + i, 1)) {
+            if (++lec >= CDC_ULTRA_LEST) return i + 8;
+            i += 8;
+            continue;
+        }
+        lec = 0;
+        const uint64_t m = r.bits(3, i >= normal ? 1 : 0, s + i, 8);
+        if (m) return i + (uint64_t)__builtin_ctzll(m);
+        i += 8;
+    }
+    return end;
+}
+
+// LeapCDC over bitmaps 0 (primary) and 1 (secondary): the 22 primary windows
+// of candidate c are bits c-22 .. c-1, the failing one nearest to c decides
+// the leap; then the two secondary windows c-23, c-24.
+__device__ uint64_t cut_leap_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+    if (n <= wp.min) return n;
+    const uint64_t end = n < wp.max ? n : wp.max;
+    uint64_t c = wp.min;
+    while (c <= end) {
+        const uint64_t z = ~r.bits(2, 0, s + c - CDC_LEAP_PRIMARY, CDC_LEAP_PRIMARY) &
+                           ((1ull << CDC_LEAP_PRIMARY) - 1);
+        if (z) {  // window k = 21 - j failed, j = the highest zero bit
+            const uint32_t j = 63u - (uint32_t)__builtin_clzll(z);
+            c += CDC_LEAP_WINDOWS - (CDC_LEAP_PRIMARY - 1 - j);
+            continue;
+        }
+        if (!r.bits(2, 1, s + c - 23, 1)) { c += CDC_LEAP_WINDOWS - 22; continue; }
+        if (!r.bits(2, 1, s + c - 24, 1)) { c += CDC_LEAP_WINDOWS - 23; continue; }
+        return c;
+    }
+    return end;
+}
+
+template <int kAlgo, bool kBits>
 __device__ __forceinline__ uint64_t cut(Reader &r, uint64_t s, uint64_t len, const WalkParams &wp, const Tabs &T) {
-    if constexpr (kAlgo == 2) return cut_rabin(r, s, len - s, wp, T);
-    else if constexpr (kAlgo == 4) return cut_ultra(r, s, len - s, wp);
-    else if constexpr (kAlgo == 5) return cut_leap(r, s, len - s, wp, T);
-    else return cut_seq(r, s, len - s, wp);
+    if constexpr (kBits) {
+        if constexpr (kAlgo == 2) return cut_rabin_bits(r, s, len - s, wp);
+        else if constexpr (kAlgo == 4) return cut_ultra_bits(r, s, len - s, wp);
+        else return cut_leap_bits(r, s, len - s, wp);
+    } else {
+        if constexpr (kAlgo == 2) return cut_rabin(r, s, len - s, wp, T);
+        else if constexpr (kAlgo == 4) return cut_ultra(r, s, len - s, wp);
+        else if constexpr (kAlgo == 5) return cut_leap(r, s, len - s, wp, T);
+        else return cut_seq(r, s, len - s, wp);
+    }
 }
 
 // Walk from chunk start c (< seg_end) to the first start >= seg_end,
 // recording the starts in the segment's list.
-template <int kAlgo>
+template <int kAlgo, bool kBits>
 __device__ void walk_from(uint64_t c, uint64_t g, uint64_t seg_end, uint64_t len, Reader &r,
                           const WalkParams &wp, const Tabs &T, const WalkState &ws) {
     ws.E[g] = c;
@@ -231,11 +328,23 @@ __device__ void walk_from(uint64_t c, uint64_t g, uint64_t seg_end, uint64_t len
     while (c < seg_end) {
         if (cnt < wp.cap) list[cnt] = c;
         ++cnt;
-        c += cut<kAlgo>(r, c, len, wp, T);
+        c += cut<kAlgo, kBits>(r, c, len, wp, T);
     }
     ws.X[g] = c;
     ws.N[g] = cnt;
     if (cnt > wp.cap) atomicAdd(&ws.flags[1], 1ull);
+}
+
+// Byte mode reads the stream; bitmap mode reads the stream's bitmap words.
+template <bool kBits>
+__device__ __forceinline__ void init_reader(Reader &r, const StreamTable &st, const WalkParams &wp, uint32_t si,
+                                            uint64_t len, uint8_t *slot) {
+    if constexpr (kBits) {
+        const uint64_t *b = wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * wp.nbm;
+        r.init(reinterpret_cast<const uint8_t *>(b), ((len + 63) >> 6) * 8ull * wp.nbm, slot);
+    } else {
+        r.init(st.ptrs[si], len, slot);
+    }
 }
 
 __device__ __forceinline__ void load_tabs(uint64_t *sh, const uint64_t *g) {
@@ -243,7 +352,7 @@ __device__ __forceinline__ void load_tabs(uint64_t *sh, const uint64_t *g) {
     __syncthreads();
 }
 
-template <int kAlgo>
+template <int kAlgo, bool kBits>
 __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, const WalkParams wp,
                                                           const WalkState ws) {
     __shared__ uint64_t tab[768];
@@ -258,19 +367,19 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
     const uint64_t len = st.lens[si];
     const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
     Reader r;
-    r.init(st.ptrs[si], len, win + threadIdx.x * kSlot);
+    init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
     // Warm-up start: `warm` bytes back, on the max-length grid of the stream
     // (so runs of max-length cuts from the stream start are in phase).
     uint64_t c = 0;
     if (off != 0) {
         c = off > wp.warm ? off - wp.warm : 0;
         c = c / wp.max * wp.max;
-        while (c < off) c += cut<kAlgo>(r, c, len, wp, T);
+        while (c < off) c += cut<kAlgo, kBits>(r, c, len, wp, T);
     }
-    walk_from<kAlgo>(c, g, seg_end, len, r, wp, T, ws);
+    walk_from<kAlgo, kBits>(c, g, seg_end, len, r, wp, T, ws);
 }
 
-template <int kAlgo>
+template <int kAlgo, bool kBits>
 __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, const WalkParams wp,
                                                          const WalkState ws) {
     __shared__ uint64_t tab[768];
@@ -288,13 +397,13 @@ __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, c
     const uint64_t len = st.lens[si];
     const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
     Reader r;
-    r.init(st.ptrs[si], len, win + threadIdx.x * kSlot);
-    walk_from<kAlgo>(x, g, seg_end, len, r, wp, T, ws);
+    init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
+    walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws);
     atomicAdd(&ws.flags[0], 1ull);
     atomicMin(&ws.flags[2], (unsigned long long)g);
 }
 
-template <int kAlgo>
+template <int kAlgo, bool kBits>
 __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st, const WalkParams wp,
                                                             const WalkState ws) {
     __shared__ uint64_t tab[768];
@@ -312,8 +421,143 @@ __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st
         const uint64_t len = st.lens[si];
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
         Reader r;
-        r.init(st.ptrs[si], len, win + threadIdx.x * kSlot);
-        walk_from<kAlgo>(x, g, seg_end, len, r, wp, T, ws);
+        init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
+        walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws);
+    }
+}
+
+// ---- bitmap pass ------------------------------------------------------------
+// Wave per segment; lane l computes the predicate bits of the positions
+// [off + l*w, off + (l+1)*w), w = segment/64 (a multiple of 64), reading its
+// bytes 16 at a time plus the window bytes before (and, for Ultra's repeat
+// test, after) its range.  Bits of positions whose window would reach before
+// the stream start are never tested by the walks (they need min >= 48 / 8 /
+// 32), nor are bits at or past the stream end.
+
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t *base, uint64_t a, uint64_t len) {
+    if (a + 16 <= len) return *reinterpret_cast<const uint4 *>(base + a);
+    uint32_t t[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)
+        if (a + j < len) t[j >> 2] |= (uint32_t)base[a + j] << (8 * (j & 3));
+    return make_uint4(t[0], t[1], t[2], t[3]);
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4 &v, int j) {
+    const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
+    return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
+__device__ __forceinline__ uint64_t lo64(const uint4 &v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint64_t hi64(const uint4 &v) { return ((uint64_t)v.w << 32) | v.z; }
+
+// The 8 bytes starting at byte o (0 <= o <= 40) of the 48 bytes W[0..5].
+__device__ __forceinline__ uint64_t window8(const uint64_t (&W)[6], int o) {
+    const int q = o >> 3, r = o & 7;
+    return r == 0 ? W[q] : (W[q] >> (8 * r)) | (W[q + 1] << (64 - 8 * r));
+}
+
+template <int kAlgo>
+__global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, const WalkParams wp) {
+    __shared__ uint64_t tab[768];
+    load_tabs(tab, wp.tabs);
+    const Tabs T{tab, tab + 256, tab + 512};
+    const uint64_t g = blockIdx.x;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint8_t *base = st.ptrs[si];
+    const uint64_t w = 1ull << (st.span_log2 - 6);
+    const uint64_t p0 = off + threadIdx.x * w;
+    if (p0 >= len) return;
+    const uint64_t p1 = min(p0 + w, len);
+    uint64_t *out = wp.bm + (g * wp.seg_words + threadIdx.x * (w >> 6)) * wp.nbm;
+    if constexpr (kAlgo == 2) {
+        // Rolling Rabin digest from 48 bytes before p0 (out bytes 0 until
+        // 48 bytes are in): the digest after byte i is the fingerprint of the
+        // window [i-47, i], exactly the digest cut_rabin tests.
+        const uint64_t f0 = p0 >= CDC_RABIN_WINDOW ? p0 - CDC_RABIN_WINDOW : 0;
+        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0;  // chunks 48, 32, 16 bytes back
+        uint64_t d = 0, acc = 0;
+        for (uint64_t a = f0; a < p1; a += 16) {
+            const uint4 cur = load16_guarded(base, a, len);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t i = a + j;
+                d ^= T.out[byte_of(c0, j)];
+                const uint64_t top = d >> wp.rabin_shift;
+                d = ((d << 8) | byte_of(cur, j)) ^ T.mod[top];
+                if (i >= p0 && i < p1) {
+                    acc |= (uint64_t)((d & wp.rabin_mask) == 0) << ((i - p0) & 63);
+                    if (((i - p0) & 63) == 63) {
+                        out[((i - p0) >> 6)] = acc;
+                        acc = 0;
+                    }
+                }
+            }
+            c0 = c1;
+            c1 = c2;
+            c2 = cur;
+        }
+        if ((p1 - p0) & 63) out[(p1 - p0) >> 6] = acc;
+    } else if constexpr (kAlgo == 4) {
+        // dist(q) = popcount of the 8 bytes before q ^ 0xAA..; repeat(q) =
+        // the 8 bytes at q equal the 8 before.  Bytes [a-16, a+32) in W.
+        constexpr uint64_t pat = 0x0101010101010101ull * CDC_ULTRA_PATTERN;
+        uint4 prev = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
+        uint4 cur = load16_guarded(base, p0, len);
+        uint64_t hs = 0, hl = 0, eq = 0;
+        for (uint64_t a = p0; a < p1; a += 16) {
+            const uint4 nxt = load16_guarded(base, a + 16, len);
+            const uint64_t W[6] = {lo64(prev), hi64(prev), lo64(cur), hi64(cur), lo64(nxt), hi64(nxt)};
+            const uint32_t sh = (uint32_t)((a - p0) & 63);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t before = window8(W, 8 + j), at = window8(W, 16 + j);
+                const uint32_t dist = (uint32_t)__popcll(before ^ pat);
+                hs |= (uint64_t)((dist & CDC_ULTRA_MASK_S) == 0) << (sh + j);
+                hl |= (uint64_t)((dist & CDC_ULTRA_MASK_L) == 0) << (sh + j);
+                eq |= (uint64_t)(before == at) << (sh + j);
+            }
+            if (sh == 48 || a + 16 >= p1) {
+                const uint64_t k = (a - p0) >> 6;
+                out[k * 3 + 0] = hs;
+                out[k * 3 + 1] = hl;
+                out[k * 3 + 2] = eq;
+                hs = hl = eq = 0;
+            }
+            prev = cur;
+            cur = nxt;
+        }
+    } else {
+        // Leap eligibility of the 5-byte window ending at p (bytes [a-16, a+16)).
+        uint4 prev = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
+        uint64_t pr = 0, se = 0;
+        for (uint64_t a = p0; a < p1; a += 16) {
+            const uint4 cur = load16_guarded(base, a, len);
+            const uint32_t sh = (uint32_t)((a - p0) & 63);
+            uint64_t e[21];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[j] = T.leap[byte_of(prev, 12 + j)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) e[4 + j] = T.leap[byte_of(cur, j)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint64_t h = 0;
+#pragma unroll
+                for (int k = 0; k < (int)CDC_LEAP_WSIZE; ++k) h += rotl64(e[4 + j - k], 11 * k);
+                pr |= (uint64_t)((uint32_t)(h >> 32) < wp.leap_thr) << (sh + j);
+                se |= (uint64_t)((uint32_t)h < wp.leap_thr) << (sh + j);
+            }
+            if (sh == 48 || a + 16 >= p1) {
+                const uint64_t k = (a - p0) >> 6;
+                out[k * 2 + 0] = pr;
+                out[k * 2 + 1] = se;
+                pr = se = 0;
+            }
+            prev = cur;
+        }
     }
 }
 
@@ -388,28 +632,39 @@ __global__ void first_kernel(const StreamTable st, const WalkState ws, uint64_t 
     ws.first[i] = g < st.total_spans ? ws.P[g] : ws.bsum[nb];
 }
 
-template <int kAlgo>
+template <int kAlgo, bool kBits>
 hipError_t walk_dispatch(int which, const StreamTable &st, const WalkParams &wp, const WalkState &ws,
                          hipStream_t s) {
     const unsigned blocks = (unsigned)((st.total_spans + kWalkBlock - 1) / kWalkBlock);
-    if (which == 0) walk_kernel<kAlgo><<<blocks, kWalkBlock, 0, s>>>(st, wp, ws);
-    else if (which == 1) fix_kernel<kAlgo><<<blocks, kWalkBlock, 0, s>>>(st, wp, ws);
-    else serial_kernel<kAlgo><<<1, kWalkBlock, 0, s>>>(st, wp, ws);
+    if (which == 0) walk_kernel<kAlgo, kBits><<<blocks, kWalkBlock, 0, s>>>(st, wp, ws);
+    else if (which == 1) fix_kernel<kAlgo, kBits><<<blocks, kWalkBlock, 0, s>>>(st, wp, ws);
+    else serial_kernel<kAlgo, kBits><<<1, kWalkBlock, 0, s>>>(st, wp, ws);
     return hipGetLastError();
 }
 
 hipError_t dispatch(int which, const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
+    const bool bits = wp.nbm != 0;
     switch (wp.algo) {
-        case 2: return walk_dispatch<2>(which, st, wp, ws, s);
-        case 4: return walk_dispatch<4>(which, st, wp, ws, s);
-        case 5: return walk_dispatch<5>(which, st, wp, ws, s);
-        case 6: return walk_dispatch<6>(which, st, wp, ws, s);
+        case 2: return bits ? walk_dispatch<2, true>(which, st, wp, ws, s) : walk_dispatch<2, false>(which, st, wp, ws, s);
+        case 4: return bits ? walk_dispatch<4, true>(which, st, wp, ws, s) : walk_dispatch<4, false>(which, st, wp, ws, s);
+        case 5: return bits ? walk_dispatch<5, true>(which, st, wp, ws, s) : walk_dispatch<5, false>(which, st, wp, ws, s);
+        case 6: return walk_dispatch<6, false>(which, st, wp, ws, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
+
+hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
+    if (!st.total_spans || !wp.nbm) return hipSuccess;
+    const unsigned blocks = (unsigned)st.total_spans;
+    if (wp.algo == 2) bits_kernel<2><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    else if (wp.algo == 4) bits_kernel<4><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    else if (wp.algo == 5) bits_kernel<5><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
 
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
     return dispatch(0, st, wp, ws, s);

@@ -1,8 +1,8 @@
 // walk.hpp -- the segment-walk engine for Rabin / UltraCDC / LeapCDC / SeqCDC
 // (reference src/chunkers/{rabin,ultra,leap,seq}.rs; DESIGN.md "Segment walk").
 //
-// Every stream of the batch is cut into segments of 2^seg_log2 bytes (>= max,
-// so no chunk spans a whole segment).  One lane owns one segment and runs the
+// Every stream of the batch is cut into segments of 2^seg_log2 bytes (a chunk
+// may span whole segments: they then hold no start, E = X).  One lane owns one segment and runs the
 // algorithm's exact byte-serial cut rule (the same rule as oracle/cdc_oracle.c)
 // from a warm-up start `warm` bytes before the segment, recording the chunk
 // starts that fall inside it.  A chain from the warm-up start usually merges
@@ -29,6 +29,12 @@ struct WalkParams {
     uint32_t cap;             // chunk starts recorded per segment
     uint64_t warm;            // warm-up bytes before a segment
     const uint64_t *tabs;     // device [768]: rabin mod[256], rabin out[256], leap hash[256]
+    // Bitmap mode (Rabin with min >= 48, Ultra, Leap): the per-position
+    // predicates of bits_kernel, nbm bitmaps interleaved per 64-bit word:
+    // word k of bitmap b of segment g at bm[(g * seg_words + k) * nbm + b].
+    uint64_t *bm;
+    uint32_t nbm;             // 0 = byte mode; Rabin 1 (hit), Ultra 3 (mask_s, mask_l, 8-byte repeat), Leap 2
+    uint32_t seg_words;       // 64-bit words per segment and bitmap (segment bytes / 64)
 };
 
 struct WalkState {
@@ -45,6 +51,8 @@ struct WalkState {
 
 constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
 
+// Bitmap mode: the predicate bitmaps of every segment (wave per segment).
+hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s);
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
 // One Jacobi round: snapshot X, then re-walk every segment whose entry is not
 // its predecessor's exit.  flags[0] counts them (the host reads it).

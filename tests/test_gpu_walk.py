@@ -168,3 +168,29 @@ def test_large_stream_device_resident(algo):
     assert_same(got, ref, f"{algo} 64 MiB")
     t = ch.last_timing()
     assert t["bytes"] == n and t["total_ms"] > 0
+
+
+@pytest.mark.parametrize("algo", ["rabin", "ultra", "leap"])
+def test_byte_mode_equals_oracle(algo, monkeypatch):
+    """The byte-serial walks (used for Rabin with min < 48, and forced here with
+    CHUNKFS_AMD_WALK_BYTES=1, read at handle creation) stay exact: the bitmap
+    mode is the default for these rules."""
+    import chunkfs_amd as c
+    monkeypatch.setenv("CHUNKFS_AMD_WALK_BYTES", "1")
+    sizes = SIZES[algo][0]
+    cls = {"rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}[algo]
+    ch = cls(c.SizeParams(*sizes))
+    for n, seed in [((1 << 20) + 5, 8), (300001, 9)]:
+        data = oracle.splitmix64_bytes(n, seed)
+        assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} byte mode n={n}")
+    data = make_input("lowentropy", 300000, 5)
+    assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} byte mode low entropy")
+    ch.close()
+
+
+@pytest.mark.parametrize("sizes", [(16, 64, 256), (40, 100, 400), (47, 2048, 8192), (48, 2048, 8192)])
+def test_rabin_small_min_byte_path(sizes):
+    """Rabin with min < 48 (partial windows at the chunk start) takes the byte
+    walks; min = 48 is the first bitmap-mode size."""
+    data = oracle.splitmix64_bytes(400003, sizes[0])
+    assert_same(chunker("rabin", sizes).chunk_array(data), oracle.cdc("rabin", data, *sizes), f"rabin {sizes}")

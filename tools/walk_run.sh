@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_walk.py -m gpu -v -x --time
     > $OUT/pytest_walk_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 $OUT/pytest_walk_$TAG.log
 [ $rc -eq 0 ] || exit $rc
-for W in default 16,4 15,2 16,2 14,4 17,4; do
+for W in ${WALKS:-default 15,4 16,8 15,16}; do
     if [ $W = default ]; then unset CHUNKFS_AMD_WALK; else export CHUNKFS_AMD_WALK=$W; fi
     timeout -k 10 120 python -u tools/walk_bench.py >> $OUT/walk_bench_$TAG.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "walk_bench $W rc=$rc"; tail -5 $OUT/walk_bench_$TAG.log; exit $rc; }
