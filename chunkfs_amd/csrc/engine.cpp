@@ -612,8 +612,8 @@ int Engine::create_walk(cdc_algo_t algo, const uint32_t seq[4], uint32_t min, ui
         set_error("invalid sizes: need 0 < min <= avg <= max (UltraCDC min >= 8, LeapCDC min >= 32)");
         return CDC_EINVAL;
     }
-    if (algo == CDC_ALGO_SEQ && (seq[0] > 1 || seq[1] == 0 || seq[2] == 0)) {
-        set_error("invalid SeqCDC config: mode 0/1, seq_length > 0, jump_trigger > 0");
+    if (algo == CDC_ALGO_SEQ && (seq[0] > 1 || seq[1] == 0 || seq[2] == 0 || seq[3] == 0)) {
+        set_error("invalid SeqCDC config: mode 0/1, seq_length > 0, jump_trigger > 0, jump_size > 0");
         return CDC_EINVAL;
     }
     Engine *e = new Engine();
@@ -675,11 +675,13 @@ int Engine::init_walk(const uint32_t *seq) {
     }
     wp.warm = warm_mult * avg_;
     wp.cap = (uint32_t)((1ull << seg_log2_) / min_ + 2);
-    // Bitmap mode for the windowed rules: Rabin when every tested
-    // digest is a full window (min >= 48), UltraCDC, LeapCDC.
-    // CHUNKFS_AMD_WALK_BYTES=1 forces the byte walks (A/B experiments).
+    // Bitmap mode: Rabin when every tested digest is a full
+    // window (min >= 48), UltraCDC, LeapCDC, and SeqCDC when its run length
+    // fits a 64-bit step (seq_length <= 63).  CHUNKFS_AMD_WALK_BYTES=1 forces
+    // the byte walks (A/B experiments).
     wp.nbm = algo_ == CDC_ALGO_RABIN ? (min_ >= CDC_RABIN_WINDOW ? 1u : 0u)
-           : algo_ == CDC_ALGO_ULTRA ? 3u : algo_ == CDC_ALGO_LEAP ? 2u : 0u;
+           : algo_ == CDC_ALGO_ULTRA ? 3u : algo_ == CDC_ALGO_LEAP ? 2u
+           : (wp.seq_len <= 63 ? 1u : 0u);
     if (const char *b = std::getenv("CHUNKFS_AMD_WALK_BYTES"))
         if (std::atoi(b) != 0) wp.nbm = 0;
     wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);

@@ -303,11 +303,52 @@ __device__ uint64_t cut_leap_bits(Reader &r, uint64_t s, uint64_t n, const WalkP
     return end;
 }
 
+// SeqCDC over bitmap 0 (pair p in the mode's direction), up to 64 positions
+// per step: a = positions where a run of seq_len in-sequence pairs completes
+// (the run carried in from the previous step included), tB = the pair at which
+// the opposing count reaches jump_trigger; the earlier event decides.
+__device__ uint64_t cut_seq_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+    if (n <= wp.min) return n;
+    const uint64_t end = n < wp.max ? n : wp.max;
+    uint32_t cnt = 0, opp = 0;
+    uint64_t i = wp.min;
+    while (i < end) {
+        const uint32_t k = (uint32_t)min(end - i, (uint64_t)64);
+        const uint64_t km = k == 64 ? ~0ull : (1ull << k) - 1;
+        const uint64_t y = r.bits(1, 0, s + i, k);
+        const uint64_t prev = cnt >= 64 ? ~0ull : cnt ? ~0ull << (64 - cnt) : 0ull;
+        uint64_t a = y;
+        for (uint32_t q = 1; q < wp.seq_len; ++q) a &= (y << q) | (prev >> (64 - q));
+        a &= km;
+        uint64_t z = ~y & km;
+        const uint32_t need = wp.seq_trig - opp;
+        uint32_t tB = 64;
+        if ((uint32_t)__popcll(z) >= need) {
+            for (uint32_t q = 1; q < need; ++q) z &= z - 1;
+            tB = (uint32_t)__builtin_ctzll(z);
+        }
+        const uint32_t tA = a ? (uint32_t)__builtin_ctzll(a) : 64u;
+        if (tA < tB) return i + tA + 1;
+        if (tB < 64) {
+            opp = 0;
+            cnt = 0;
+            i += tB + wp.seq_jump;
+            continue;
+        }
+        opp += (uint32_t)__popcll(~y & km);
+        const uint64_t zz = ~y & km;
+        cnt = zz ? k - 1 - (63u - (uint32_t)__builtin_clzll(zz)) : min(cnt + k, 1u << 30);
+        i += k;
+    }
+    return end;
+}
+
 template <int kAlgo, bool kBits>
 __device__ __forceinline__ uint64_t cut(Reader &r, uint64_t s, uint64_t len, const WalkParams &wp, const Tabs &T) {
     if constexpr (kBits) {
         if constexpr (kAlgo == 2) return cut_rabin_bits(r, s, len - s, wp);
         else if constexpr (kAlgo == 4) return cut_ultra_bits(r, s, len - s, wp);
+        else if constexpr (kAlgo == 6) return cut_seq_bits(r, s, len - s, wp);
         else return cut_leap_bits(r, s, len - s, wp);
     } else {
         if constexpr (kAlgo == 2) return cut_rabin(r, s, len - s, wp, T);
@@ -530,6 +571,24 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             prev = cur;
             cur = nxt;
         }
+    } else if constexpr (kAlgo == 6) {
+        // SeqCDC: bit p = (b[p] > b[p-1]) (increasing) or (b[p] < b[p-1]).
+        uint32_t last = p0 >= 1 ? base[p0 - 1] : 0u;
+        uint64_t acc = 0;
+        for (uint64_t a = p0; a < p1; a += 16) {
+            const uint4 cur = load16_guarded(base, a, len);
+            const uint32_t sh = (uint32_t)((a - p0) & 63);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t b = byte_of(cur, j);
+                acc |= (uint64_t)(wp.seq_mode ? b < last : b > last) << (sh + j);
+                last = b;
+            }
+            if (sh == 48 || a + 16 >= p1) {
+                out[(a - p0) >> 6] = acc;
+                acc = 0;
+            }
+        }
     } else {
         // Leap eligibility of the 5-byte window ending at p (bytes [a-16, a+16)).
         uint4 prev = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
@@ -649,7 +708,7 @@ hipError_t dispatch(int which, const StreamTable &st, const WalkParams &wp, cons
         case 2: return bits ? walk_dispatch<2, true>(which, st, wp, ws, s) : walk_dispatch<2, false>(which, st, wp, ws, s);
         case 4: return bits ? walk_dispatch<4, true>(which, st, wp, ws, s) : walk_dispatch<4, false>(which, st, wp, ws, s);
         case 5: return bits ? walk_dispatch<5, true>(which, st, wp, ws, s) : walk_dispatch<5, false>(which, st, wp, ws, s);
-        case 6: return walk_dispatch<6, false>(which, st, wp, ws, s);
+        case 6: return bits ? walk_dispatch<6, true>(which, st, wp, ws, s) : walk_dispatch<6, false>(which, st, wp, ws, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -662,6 +721,7 @@ hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t 
     if (wp.algo == 2) bits_kernel<2><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 4) bits_kernel<4><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 5) bits_kernel<5><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    else if (wp.algo == 6) bits_kernel<6><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -428,7 +428,7 @@ int64_t oracle_cdc_chunk(int algo, const uint8_t *data, uint64_t len, uint32_t m
     }
     const uint32_t defcfg[4] = {0, CDC_SEQ_LENGTH, CDC_SEQ_JUMP_TRIGGER, CDC_SEQ_JUMP_SIZE};
     const uint32_t *cfg = seqcfg ? seqcfg : defcfg;
-    if (algo == 6 && (cfg[1] == 0 || cfg[2] == 0)) return -1;
+    if (algo == 6 && (cfg[0] > 1 || cfg[1] == 0 || cfg[2] == 0 || cfg[3] == 0)) return -1;
     const uint64_t rmask = (1ull << cdc_log2_round(avg)) - 1;
     const uint32_t thr = oracle_leap_threshold(min, avg);
     uint64_t processed = 0, count = 0;

@@ -105,6 +105,9 @@ def test_walk_chunkers_reject_bad_sizes_before_device():
     with pytest.raises(c.CdcError) as ei:
         c.SeqChunker(c.OperationMode.Decreasing, c.SizeParams(64, 128, 256), c.SeqConfig(0, 50, 256))
     assert ei.value.code == -1
+    with pytest.raises(c.CdcError) as ei:
+        c.SeqChunker(c.OperationMode.Increasing, c.SizeParams(64, 128, 256), c.SeqConfig(5, 1, 0))
+    assert ei.value.code == -1
 
 
 def test_python_mirror_debug_strings():

@@ -170,7 +170,7 @@ def test_large_stream_device_resident(algo):
     assert t["bytes"] == n and t["total_ms"] > 0
 
 
-@pytest.mark.parametrize("algo", ["rabin", "ultra", "leap"])
+@pytest.mark.parametrize("algo", ["rabin", "ultra", "leap", "seq"])
 def test_byte_mode_equals_oracle(algo, monkeypatch):
     """The byte-serial walks (used for Rabin with min < 48, and forced here with
     CHUNKFS_AMD_WALK_BYTES=1, read at handle creation) stay exact: the bitmap
@@ -178,8 +178,8 @@ def test_byte_mode_equals_oracle(algo, monkeypatch):
     import chunkfs_amd as c
     monkeypatch.setenv("CHUNKFS_AMD_WALK_BYTES", "1")
     sizes = SIZES[algo][0]
-    cls = {"rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}[algo]
-    ch = cls(c.SizeParams(*sizes))
+    cls = {"rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}.get(algo)
+    ch = cls(c.SizeParams(*sizes)) if cls else c.SeqChunker(0, c.SizeParams(*sizes))
     for n, seed in [((1 << 20) + 5, 8), (300001, 9)]:
         data = oracle.splitmix64_bytes(n, seed)
         assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} byte mode n={n}")
@@ -194,3 +194,19 @@ def test_rabin_small_min_byte_path(sizes):
     walks; min = 48 is the first bitmap-mode size."""
     data = oracle.splitmix64_bytes(400003, sizes[0])
     assert_same(chunker("rabin", sizes).chunk_array(data), oracle.cdc("rabin", data, *sizes), f"rabin {sizes}")
+
+
+def test_seq_bitmap_long_runs_and_configs():
+    """SeqCDC's word-at-a-time walk: runs and opposing counts carried across
+    64-bit steps (ramps, short periods), long seq_length, jump_trigger 1."""
+    import chunkfs_amd as c
+    ramp = (np.arange(700000) % 256).astype(np.uint8)          # long increasing runs
+    saw = (np.arange(700000) % 7).astype(np.uint8)            # runs of 6, then a drop
+    rnd = oracle.splitmix64_bytes(700001, 77)
+    for data in (ramp, saw, rnd):
+        for mode, cfg in [(0, c.SeqConfig(5, 50, 256)), (1, c.SeqConfig(5, 50, 256)), (0, c.SeqConfig(63, 1, 3)),
+                          (0, c.SeqConfig(6, 100, 1)), (1, c.SeqConfig(2, 64, 65)), (0, c.SeqConfig(64, 5, 10))]:
+            ch = c.SeqChunker(mode, c.SizeParams(300, 1000, 5000), cfg)
+            ref = oracle.cdc("seq", data, 300, 1000, 5000, seqcfg=(mode, cfg.seq_length, cfg.jump_trigger, cfg.jump_size))
+            assert_same(ch.chunk_array(data), ref, f"seq mode={mode} {cfg}")
+            ch.close()
