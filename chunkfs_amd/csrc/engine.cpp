@@ -760,12 +760,12 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     uint64_t rewalked = 0;
     bool settled = false;
     for (uint32_t r = 0; r < max_rounds_ && !settled; ++r) {
-        HIP_TRY(hipMemsetAsync(wst_.flags, 0, 8, s));         // segments re-walked
-        HIP_TRY(hipMemsetAsync(wst_.flags + 2, 0xFF, 8, s));  // lowest re-walked segment
+        HIP_TRY(hipMemsetAsync(wst_.flags, 0, 8, s));         // exits changed this round
+        HIP_TRY(hipMemsetAsync(wst_.flags + 2, 0xFF, 8, s));  // lowest segment whose exit changed
         HIP_TRY(walk::launch_fix(st, wp_, wst_, s));
         HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        rewalked += h_flags[0];
+        rewalked = h_flags[3];
         settled = h_flags[0] == 0;
     }
     // Chains that never merge (periodic data): one exact in-order pass from

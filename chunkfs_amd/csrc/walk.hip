@@ -376,6 +376,53 @@ __device__ void walk_from(uint64_t c, uint64_t g, uint64_t seg_end, uint64_t len
     if (cnt > wp.cap) atomicAdd(&ws.flags[1], 1ull);
 }
 
+// Re-walk of segment g from x (a fix-up): the new chain usually meets the
+// segment's old chain within a few chunks, and from a common start on the two
+// are the same chain, so the old tail and exit stay.  Up to kNew new starts are
+// held in the lane's LDS slots; then the old list is shifted behind them.
+// Without a meeting point within kNew starts: a full walk_from.  Returns
+// whether the exit X changed (only then can successors be affected).
+constexpr uint32_t kNew = 8;
+
+template <int kAlgo, bool kBits>
+__device__ bool rewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, Reader &r, const WalkParams &wp,
+                       const Tabs &T, const WalkState &ws, uint64_t *nb) {
+    uint64_t *list = ws.list + g * wp.cap;
+    const uint32_t n_old = ws.N[g];
+    const uint32_t lim = min(n_old, wp.cap);
+    const uint64_t x_old = ws.X[g];
+    uint64_t c = x;
+    uint32_t m = 0, j = 0;
+    while (c < seg_end && m < kNew) {
+        while (j < lim && list[j] < c) ++j;
+        if (j < lim && list[j] == c) {  // meets the old chain at old start j
+            if (m < j) {
+                for (uint32_t k = j; k < lim; ++k) list[m + k - j] = list[k];
+            } else if (m > j) {
+                for (uint32_t k = lim; k-- > j;)
+                    if (m + k - j < wp.cap) list[m + k - j] = list[k];
+            }
+            for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
+            ws.E[g] = x;
+            ws.N[g] = m + (n_old - j);
+            if (m + (n_old - j) > wp.cap) atomicAdd(&ws.flags[1], 1ull);
+            return false;
+        }
+        nb[m++] = c;
+        c += cut<kAlgo, kBits>(r, c, len, wp, T);
+    }
+    if (c >= seg_end) {  // the whole segment in <= kNew starts, no meeting point
+        for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
+        ws.E[g] = x;
+        ws.N[g] = m;
+        ws.X[g] = c;
+        return c != x_old;
+    }
+    walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws);
+    return ws.X[g] != x_old;
+}
+
+
 // Byte mode reads the stream; bitmap mode reads the stream's bitmap words.
 template <bool kBits>
 __device__ __forceinline__ void init_reader(Reader &r, const StreamTable &st, const WalkParams &wp, uint32_t si,
@@ -425,6 +472,7 @@ __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, c
                                                          const WalkState ws) {
     __shared__ uint64_t tab[768];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWalkBlock * kSlot];
+    __shared__ uint64_t nbuf[kWalkBlock * kNew];
     load_tabs(tab, wp.tabs);
     const Tabs T{tab, tab + 256, tab + 512};
     const uint64_t g = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
@@ -439,9 +487,11 @@ __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, c
     const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
     Reader r;
     init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
-    walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws);
-    atomicAdd(&ws.flags[0], 1ull);
-    atomicMin(&ws.flags[2], (unsigned long long)g);
+    atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
+    if (rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf + threadIdx.x * kNew)) {
+        atomicAdd(&ws.flags[0], 1ull);  // exits changed: another round
+        atomicMin(&ws.flags[2], (unsigned long long)g);
+    }
 }
 
 template <int kAlgo, bool kBits>
@@ -449,6 +499,7 @@ __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st
                                                             const WalkState ws) {
     __shared__ uint64_t tab[768];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWalkBlock * kSlot];
+    __shared__ uint64_t nbuf[kNew];
     load_tabs(tab, wp.tabs);
     const Tabs T{tab, tab + 256, tab + 512};
     if (threadIdx.x != 0) return;
@@ -463,7 +514,7 @@ __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
         Reader r;
         init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
-        walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws);
+        (void)rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf);
     }
 }
 
@@ -498,6 +549,27 @@ __device__ __forceinline__ uint64_t window8(const uint64_t (&W)[6], int o) {
     return r == 0 ? W[q] : (W[q] >> (8 * r)) | (W[q + 1] << (64 - 8 * r));
 }
 
+// The lane's 16-byte chunks [a0, a1) in order, 64 bytes per step with the
+// next 64 bytes' loads in flight while f(chunk, address) runs.
+template <typename F>
+__device__ __forceinline__ void for_chunks(const uint8_t *base, uint64_t len, uint64_t a0, uint64_t a1, F &&f) {
+    uint4 n0 = load16_guarded(base, a0, len), n1 = load16_guarded(base, a0 + 16, len);
+    uint4 n2 = load16_guarded(base, a0 + 32, len), n3 = load16_guarded(base, a0 + 48, len);
+    for (uint64_t a = a0; a < a1; a += 64) {
+        const uint4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+        if (a + 64 < a1) {
+            n0 = load16_guarded(base, a + 64, len);
+            n1 = load16_guarded(base, a + 80, len);
+            n2 = load16_guarded(base, a + 96, len);
+            n3 = load16_guarded(base, a + 112, len);
+        }
+        f(c0, a);
+        if (a + 16 < a1) f(c1, a + 16);
+        if (a + 32 < a1) f(c2, a + 32);
+        if (a + 48 < a1) f(c3, a + 48);
+    }
+}
+
 template <int kAlgo>
 __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, const WalkParams wp) {
     __shared__ uint64_t tab[768];
@@ -521,8 +593,7 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
         const uint64_t f0 = p0 >= CDC_RABIN_WINDOW ? p0 - CDC_RABIN_WINDOW : 0;
         uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0;  // chunks 48, 32, 16 bytes back
         uint64_t d = 0, acc = 0;
-        for (uint64_t a = f0; a < p1; a += 16) {
-            const uint4 cur = load16_guarded(base, a, len);
+        for_chunks(base, len, f0, p1, [&](const uint4 &cur, uint64_t a) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const uint64_t i = a + j;
@@ -540,17 +611,22 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             c0 = c1;
             c1 = c2;
             c2 = cur;
-        }
+        });
         if ((p1 - p0) & 63) out[(p1 - p0) >> 6] = acc;
     } else if constexpr (kAlgo == 4) {
         // dist(q) = popcount of the 8 bytes before q ^ 0xAA..; repeat(q) =
-        // the 8 bytes at q equal the 8 before.  Bytes [a-16, a+32) in W.
+        // the 8 bytes at q equal the 8 before.  A chunk's positions are
+        // evaluated when the chunk after it arrives (bytes [a-16, a+32) in W).
         constexpr uint64_t pat = 0x0101010101010101ull * CDC_ULTRA_PATTERN;
         uint4 prev = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
-        uint4 cur = load16_guarded(base, p0, len);
+        uint4 cur = make_uint4(0, 0, 0, 0);
         uint64_t hs = 0, hl = 0, eq = 0;
-        for (uint64_t a = p0; a < p1; a += 16) {
-            const uint4 nxt = load16_guarded(base, a + 16, len);
+        for_chunks(base, len, p0, p1 + 16, [&](const uint4 &nxt, uint64_t an) {
+            if (an == p0) {
+                cur = nxt;
+                return;
+            }
+            const uint64_t a = an - 16;  // the chunk evaluated now
             const uint64_t W[6] = {lo64(prev), hi64(prev), lo64(cur), hi64(cur), lo64(nxt), hi64(nxt)};
             const uint32_t sh = (uint32_t)((a - p0) & 63);
 #pragma unroll
@@ -570,13 +646,12 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             }
             prev = cur;
             cur = nxt;
-        }
+        });
     } else if constexpr (kAlgo == 6) {
         // SeqCDC: bit p = (b[p] > b[p-1]) (increasing) or (b[p] < b[p-1]).
         uint32_t last = p0 >= 1 ? base[p0 - 1] : 0u;
         uint64_t acc = 0;
-        for (uint64_t a = p0; a < p1; a += 16) {
-            const uint4 cur = load16_guarded(base, a, len);
+        for_chunks(base, len, p0, p1, [&](const uint4 &cur, uint64_t a) {
             const uint32_t sh = (uint32_t)((a - p0) & 63);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
@@ -588,13 +663,12 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
                 out[(a - p0) >> 6] = acc;
                 acc = 0;
             }
-        }
+        });
     } else {
         // Leap eligibility of the 5-byte window ending at p (bytes [a-16, a+16)).
         uint4 prev = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
         uint64_t pr = 0, se = 0;
-        for (uint64_t a = p0; a < p1; a += 16) {
-            const uint4 cur = load16_guarded(base, a, len);
+        for_chunks(base, len, p0, p1, [&](const uint4 &cur, uint64_t a) {
             const uint32_t sh = (uint32_t)((a - p0) & 63);
             uint64_t e[21];
 #pragma unroll
@@ -616,7 +690,7 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
                 pr = se = 0;
             }
             prev = cur;
-        }
+        });
     }
 }
 

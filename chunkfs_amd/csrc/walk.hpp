@@ -46,7 +46,7 @@ struct WalkState {
     uint64_t *P;      // [S + 1] exclusive prefix of N (chunk index of each segment)
     uint64_t *bsum;   // [blocks + 1] per-block sums of the prefix
     uint64_t *first;  // [n + 1] chunk index of each stream's first chunk
-    unsigned long long *flags;  // [4]: 0 segments re-walked this round, 1 errors, 2 lowest re-walked segment
+    unsigned long long *flags;  // [4]: 0 exits changed this round, 1 errors, 2 lowest such segment, 3 re-walks
 };
 
 constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
@@ -55,7 +55,8 @@ constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s);
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
 // One Jacobi round: snapshot X, then re-walk every segment whose entry is not
-// its predecessor's exit.  flags[0] counts them (the host reads it).
+// its predecessor's exit, stopping where the new chain meets the old one.
+// flags[0] counts the re-walks that changed an exit (the host loops while > 0).
 hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
 // Exact in-order pass over all segments from the lowest one re-walked.
 hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
