@@ -70,6 +70,12 @@ def parse(argv=None):
                    help="skip the one-off host-buffer (PCIe-inclusive) rates")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU launcher test only
+    # Multi-rank rehearsal on a box with fewer GPUs than ranks (tests only):
+    # gloo collectives, ranks mapped onto the visible devices round-robin, and
+    # every rank checks its own first streams against the oracle.
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
+    p.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--rank-parity", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args(argv)
     if a.workload is None:
         a.workload = "stream" if a.gpus == 1 else "batch"
@@ -518,11 +524,17 @@ def main(argv=None):
         if world > 1:
             dist.init_process_group("gloo")
     else:
+        if args.share_device:
+            local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         if world > 1:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if args.dist_backend == "gloo":
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         eng = DeviceEngine(args, local)
     dev = eng.dev
+    red_dev = None if (args.stub or args.dist_backend == "gloo") else dev  # where reductions run
 
     if args.workload == "stream":
         shard = sharding.stream_shard(rank, world, args.stream_bytes)
@@ -549,14 +561,14 @@ def main(argv=None):
     eng.sync()
     if world > 1:
         dist.barrier()
-    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, dev)
+    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, red_dev)
 
     bytes_rank = sum(shard.lens)
-    total_bytes = sharding.sum_over_ranks(bytes_rank, dev) * args.steps
+    total_bytes = sharding.sum_over_ranks(bytes_rank, red_dev) * args.steps
     value = sharding.aggregate_gibps(total_bytes, elapsed)
     scan_avg_ms = sum(scan_ms) / len(scan_ms)
     nchunks = int(first[-1])
-    total_chunks = sharding.sum_over_ranks(nchunks, dev)
+    total_chunks = sharding.sum_over_ranks(nchunks, red_dev)
     ms_per_step = elapsed / args.steps * 1e3
     achieved = bytes_rank / (scan_avg_ms * 1e-3) / 1e9 if scan_avg_ms > 0 else None
     e2e = bytes_rank / (ms_per_step * 1e-3) / 1e9  # per-GPU bytes / wall step time
@@ -596,6 +608,16 @@ def main(argv=None):
             fw = extras.get("host_path", {}).get("fs_write_1MiB_segments")
             if fw:
                 fw["x_cpu_single_thread"] = fw["GiBps"] / extras["cpu_baseline"]["value"]
+
+    if args.rank_parity and not args.stub:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        ok = 1
+        for i in range(min(len(shard.lens), 2)):
+            got = eng.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
+            ref = oracle.fastcdc(eng.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
+            ok &= int(got.shape == ref.shape and bool((got == ref).all()))
+        extras["parity_all_ranks"] = bool(sharding.min_over_ranks(ok, red_dev)) if world > 1 else bool(ok)
 
     traffic, traffic_src = traffic_for_build(args.traffic_json, bytes_rank)
     if rank == 0:

@@ -56,6 +56,17 @@ def sum_over_ranks(value: int, device=None) -> int:
     return int(t.item())
 
 
+def min_over_ranks(value: int, device=None) -> int:
+    """Min of a per-rank integer (e.g. a 0/1 check) across the process group."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return int(value)
+    t = torch.tensor([int(value)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
 def aggregate_gibps(total_bytes: int, elapsed_max_s: float) -> float:
     """Whole-job throughput: bytes all ranks processed / max-over-ranks time."""
     return total_bytes / elapsed_max_s / (1 << 30)

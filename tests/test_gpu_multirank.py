@@ -1,0 +1,31 @@
+"""The N>1 bench path on the HIP engine (-m gpu): `bench.py --gpus 2` starts two
+ranks itself; on a one-GPU box both share cuda:0 (--share-device) and the
+timing / byte reductions run over gloo (--dist-backend gloo) -- on an 8-GPU node
+the driver runs the same path with one GPU per rank over RCCL.  Each rank chunks
+its own block of the config-4 batch with no data-path collective and checks its
+first streams bit-exact against the oracle (--rank-parity, min over ranks)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_ranks_on_hip_engine():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
+                        "--dist-backend", "gloo", "--rank-parity", "--workload", "batch", "--batch-streams", "8",
+                        "--batch-stream-bytes", str(8 << 20), "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["streams_per_gpu"] == 4
+    assert line["parity_all_ranks"] is True
+    assert line["value"] > 0
