@@ -665,6 +665,10 @@ int Engine::init_walk(const uint32_t *seq) {
     // start merges with the true one within a few content-defined cuts).
     const uint32_t l2 = ceil_log2(avg_) + 2;
     seg_log2_ = l2 < 15 ? 15 : l2;
+    // The per-segment start list holds segment/min + 2 entries: keep it <= ~4k
+    // (tiny min), and segments >= 4 KiB.
+    const uint32_t lmin = 63 - (uint32_t)__builtin_clzll((uint64_t)min_) + 12;
+    if (seg_log2_ > lmin) seg_log2_ = lmin < 12 ? 12 : lmin;
     uint64_t warm_mult = 8;
     if (const char *w = std::getenv("CHUNKFS_AMD_WALK")) {
         unsigned a = 0, b = 0;

@@ -210,3 +210,34 @@ def test_seq_bitmap_long_runs_and_configs():
             ref = oracle.cdc("seq", data, 300, 1000, 5000, seqcfg=(mode, cfg.seq_length, cfg.jump_trigger, cfg.jump_size))
             assert_same(ch.chunk_array(data), ref, f"seq mode={mode} {cfg}")
             ch.close()
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_many_small_streams_batch(algo):
+    """2000 streams of 0..40000 bytes in one device batch: per-stream segment
+    tables, bitmap offsets and stream-end handling in every kernel."""
+    import torch
+    sizes = SIZES[algo][1]
+    rng = np.random.default_rng(11)
+    lens = [int(x) for x in rng.integers(0, 40000, 2000)]
+    lens[::97] = [0] * len(lens[::97])
+    host = oracle.splitmix64_bytes(sum(lens) + 16, 2024)
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    # one device buffer, each stream 16-byte aligned inside it
+    starts, pos = [], 0
+    for n in lens:
+        starts.append(pos)
+        pos += (n + 15) // 16 * 16 + 16
+    dev = torch.zeros(pos + 16, dtype=torch.uint8, device="cuda:0")
+    for i, n in enumerate(lens):
+        if n:
+            dev[starts[i]:starts[i] + n] = torch.from_numpy(host[offs[i]:offs[i] + n].copy()).to("cuda:0")
+    ch = chunker(algo, sizes)
+    cap = ch.batch_max_chunks(lens)
+    out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    first = ch.chunk_batch_device([dev.data_ptr() + s for s in starts], lens, out.data_ptr(), cap)
+    got = out.cpu().numpy().astype(np.uint64)
+    for i, n in enumerate(lens):
+        ref = oracle.cdc(algo, host[offs[i]:offs[i] + n], *sizes)
+        assert_same(got[first[i]:first[i + 1]], ref, f"{algo} stream {i} len {n}")
