@@ -128,12 +128,16 @@ class DeviceEngine:
             self.bufs.append(b)
         self.lens = list(lens)
         self.ptrs = [b.data_ptr() for b in self.bufs]
+        import numpy as np
+        self.ptrs_a = np.array(self.ptrs, dtype=np.uint64)  # converted once, not per step
+        self.lens_a = np.array(self.lens, dtype=np.uint64)
         self.cap = self.ch.batch_max_chunks(self.lens)
         self.out = torch.empty((max(self.cap, 1), 2), dtype=torch.int64, device=self.dev)
+        self.out_ptr = self.out.data_ptr()
         torch.cuda.synchronize()
 
     def step(self):
-        return self.ch.chunk_batch_device(self.ptrs, self.lens, self.out.data_ptr(), self.cap)
+        return self.ch.chunk_batch_device(self.ptrs_a, self.lens_a, self.out_ptr, self.cap)
 
     def timing(self):
         return self.ch.last_timing()

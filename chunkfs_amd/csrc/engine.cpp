@@ -374,6 +374,16 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     HIP_TRY(hipEventRecord(ev_[1], s));
     HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, ch3_, cp, rs, d_out, out_cap_, s));
     HIP_TRY(hipEventRecord(ev_[2], s));
+    // The resolve's last block writes the done word into coherent pinned
+    // memory after a system-scope fence: spin on it (wakes faster than a
+    // blocking stream sync), bounded, then the stream sync confirms.
+    {
+        const volatile uint64_t *done = h_misc + p3::kStatDone;
+        const auto t_spin = std::chrono::steady_clock::now();
+        while (*done == ~0ull &&
+               std::chrono::steady_clock::now() - t_spin < std::chrono::milliseconds(200)) {
+        }
+    }
     HIP_TRY(hipStreamSynchronize(s));
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
         set_error(h_misc[p3::kStatDone] != 1 ? "resolve kernel did not report back"
