@@ -1,8 +1,8 @@
 /*
  * chunkfs_amd_debug.h -- diagnostic entry points (not part of the drop-in
  * boundary).  They expose intermediate arrays of the LAST FastCDC batch of a
- * handle so the two pipelines can be compared stage by stage on a GPU
- * (tests/test_gpu_pipeline2.py, tools/validate_pipeline2.sh).
+ * handle, so the scan's candidate records can be checked stage by stage on a
+ * GPU (tests/test_gpu_resolve_paths.py).
  */
 #ifndef CHUNKFS_AMD_DEBUG_H
 #define CHUNKFS_AMD_DEBUG_H
@@ -20,9 +20,8 @@ uint32_t cdc_debug_record_cap(const cdc_handle_t *h);
 /* Copy array `what` of the last batch to host memory `out` (at most
  * max_bytes): 0 = per-span candidate counts (u32; > cap means overflowed),
  * 1 = candidate records (u32, cap per span: offset in span | bit30 mask_l
- * hit | bit31 mask_s hit; pipeline 1 also keeps its truncated-region result
- * in bits 24..29), 2 = pipeline 2's record links (u64, cap per span).
- * Returns the bytes copied or a negative CDC_E* code. */
+ * hit | bit31 mask_s hit).  Returns the bytes copied or a negative CDC_E*
+ * code (CDC_EINVAL for any other `what`). */
 int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes);
 
 #ifdef __cplusplus
