@@ -688,6 +688,17 @@ int Engine::init_walk(const uint32_t *seq) {
         }
     }
     wp.warm = warm_mult * avg_;
+    // CHUNKFS_AMD_AHEAD="after,max" overrides the run-ahead schedule (experiments).
+    if (const char *a = std::getenv("CHUNKFS_AMD_AHEAD")) {
+        unsigned x = 0, y = 0;
+        if (std::sscanf(a, "%u,%u", &x, &y) == 2 && y >= 1) {
+            ahead_after_ = x;
+            ahead_max_ = y;
+        }
+    }
+    wp.ahead = 1;
+    wp.bits_fine = 1;
+    if (const char *f = std::getenv("CHUNKFS_AMD_BITS_FINE")) wp.bits_fine = std::atoi(f) != 0 ? 1u : 0u;
     wp.cap = (uint32_t)((1ull << seg_log2_) / min_ + 2);
     // Bitmap mode: Rabin when every tested digest is a full
     // window (min >= 48), UltraCDC, LeapCDC, and SeqCDC when its run length
@@ -730,7 +741,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
         off = align_up(off + bytes, A);
         return o;
     };
-    const size_t oE = take(S * 8), oX = take(S * 8), oXs = take(S * 8), oP = take((S + 1) * 8);
+    const size_t oE = take(S * 8), oX = take(S * 8), oXs = take(S * 8), oEs = take(S * 8), oP = take((S + 1) * 8);
     const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
     const size_t oF = take((N + 1) * 8), oG = take(4 * 8);
     const size_t oBM = take(S * (size_t)wp_.seg_words * wp_.nbm * 8);  // predicate bitmaps
@@ -747,6 +758,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wst_.E = reinterpret_cast<uint64_t *>(b + oE);
     wst_.X = reinterpret_cast<uint64_t *>(b + oX);
     wst_.Xs = reinterpret_cast<uint64_t *>(b + oXs);
+    wst_.Es = reinterpret_cast<uint64_t *>(b + oEs);
     wst_.P = reinterpret_cast<uint64_t *>(b + oP);
     wst_.N = reinterpret_cast<uint32_t *>(b + oN);
     wst_.list = reinterpret_cast<uint64_t *>(b + oL);
@@ -774,6 +786,10 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     uint64_t rewalked = 0;
     bool settled = false;
     for (uint32_t r = 0; r < max_rounds_ && !settled; ++r) {
+        // Plain Jacobi for the first ahead_after_ rounds, then run-ahead
+        // re-walks (walk.hip fix_kernel) so long non-merging stretches settle
+        // before the serial pass would be needed.
+        wp_.ahead = r < ahead_after_ ? 1u : ahead_max_;
         HIP_TRY(hipMemsetAsync(wst_.flags, 0, 8, s));         // exits changed this round
         HIP_TRY(hipMemsetAsync(wst_.flags + 2, 0xFF, 8, s));  // lowest segment whose exit changed
         HIP_TRY(walk::launch_fix(st, wp_, wst_, s));

@@ -141,6 +141,8 @@ class Engine {
     walk::WalkParams wp_{};
     uint32_t seg_log2_ = 14;
     uint32_t max_rounds_ = 16;     // Jacobi fix-up rounds before the serial pass
+    uint32_t ahead_after_ = 8;     // rounds of plain Jacobi before run-ahead re-walks
+    uint32_t ahead_max_ = 64;      // segments one lane may re-walk in a run-ahead round
     uint64_t *d_wtabs_ = nullptr;  // [768] rabin mod/out + leap hash tables
     void *wws_ = nullptr;          // walk workspace arena (grow-only)
     uint64_t wws_segs_ = 0;

@@ -9,7 +9,8 @@
 //
 // Kernels, one launch each, all on the handle's stream:
 //   walk_kernel    lane per segment: warm-up walk, then the segment's starts
-//   fix_kernel     lane per segment: re-walk where entry != predecessor exit
+//   fix_kernel     lane per segment: re-walk where entry != predecessor exit,
+//                  running ahead into unscheduled successors
 //   serial_kernel  one lane: in-order re-walk from the lowest changed segment
 //   sum/scan/emit  block sums of N -> block prefix -> per-segment prefix and
 //                  the Chunk{offset,length} output; first[] per stream
@@ -41,34 +42,45 @@ __device__ __forceinline__ void locate(const StreamTable &st, uint64_t g, uint32
 // pays one memory latency per >= kWin - kBack - 16 bytes of progress instead
 // of one per divergent 16-byte miss.  Bytes past the stream end read as 0 and
 // are never loaded.
-constexpr uint32_t kWin = 256;                // window bytes per lane
+constexpr uint32_t kWin = 1024;               // window bytes per lane
 constexpr uint32_t kBack = 64;                // bytes kept behind the position at a refill
 constexpr uint32_t kSlot = kWin + 16;         // LDS stride per lane (bank spread)
 
 // Refill of one lane's window (out of line: one copy per kernel, called from
-// every read site); returns the new window start.
+// every read site); returns the new window start.  The window is loaded in
+// batches of 16 global_load_dwordx4 with the next batch in flight while the
+// previous one is written to LDS (64 + 64 VGPRs, no spills at kWin = 1 KiB).
+constexpr uint32_t kBatch = 16;
+
+__device__ __forceinline__ uint4 load_piece(const uint8_t *base, uint64_t len, uint64_t a) {
+    if (a + 16 <= len) return *reinterpret_cast<const uint4 *>(base + a);
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    for (uint32_t j = 0; a + j < len && j < 16; ++j) {
+        const uint32_t x = (uint32_t)base[a + j] << (8 * (j & 3));
+        if (j < 4) t0 |= x;
+        else if (j < 8) t1 |= x;
+        else if (j < 12) t2 |= x;
+        else t3 |= x;
+    }
+    return make_uint4(t0, t1, t2, t3);
+}
+
 __device__ __noinline__ uint64_t refill_window(const uint8_t *base, uint64_t len, uint8_t *slot, uint64_t p) {
     const uint64_t w0 = (p > kBack ? p - kBack : 0) & ~15ull;
-    uint4 v[kWin / 16];
+    constexpr uint32_t nb = kWin / 16 / kBatch;
+    uint4 v[2][kBatch];
 #pragma unroll
-    for (uint32_t k = 0; k < kWin / 16; ++k) {
-        const uint64_t a = w0 + 16 * k;
-        if (a + 16 <= len) {
-            v[k] = *reinterpret_cast<const uint4 *>(base + a);
-        } else {
-            uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-            for (uint32_t j = 0; a + j < len && j < 16; ++j) {
-                const uint32_t x = (uint32_t)base[a + j] << (8 * (j & 3));
-                if (j < 4) t0 |= x;
-                else if (j < 8) t1 |= x;
-                else if (j < 12) t2 |= x;
-                else t3 |= x;
-            }
-            v[k] = make_uint4(t0, t1, t2, t3);
+    for (uint32_t k = 0; k < kBatch; ++k) v[0][k] = load_piece(base, len, w0 + 16 * k);
+#pragma unroll
+    for (uint32_t b = 0; b < nb; ++b) {
+        if (b + 1 < nb) {
+#pragma unroll
+            for (uint32_t k = 0; k < kBatch; ++k)
+                v[(b + 1) & 1][k] = load_piece(base, len, w0 + 16 * ((b + 1) * kBatch + k));
         }
-    }
 #pragma unroll
-    for (uint32_t k = 0; k < kWin / 16; ++k) reinterpret_cast<uint4 *>(slot)[k] = v[k];
+        for (uint32_t k = 0; k < kBatch; ++k) reinterpret_cast<uint4 *>(slot)[b * kBatch + k] = v[b & 1][k];
+    }
     return w0;
 }
 
@@ -467,6 +479,15 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
     walk_from<kAlgo, kBits>(c, g, seg_end, len, r, wp, T, ws);
 }
 
+// One Jacobi round.  Segment g is scheduled when its entry differs from its
+// predecessor's exit in the round's snapshots (Es, Xs).  A lane whose re-walk
+// changes the exit runs ahead into the successor when that one is NOT
+// scheduled (no other lane touches it this round), and on until the chains
+// meet, the stream ends, a scheduled successor, or wp.ahead segments: chains
+// that take several segments to merge (SeqCDC's jumps) settle in one launch
+// instead of one round per segment.  Scheduling reads only the snapshots, so a
+// run-ahead write of E[g+1] never makes lane g+1 re-walk concurrently.
+
 template <int kAlgo, bool kBits>
 __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, const WalkParams wp,
                                                          const WalkState ws) {
@@ -481,16 +502,26 @@ __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, c
     uint64_t off;
     locate(st, g, si, off);
     if (off == 0) return;  // a stream's first segment starts exactly at 0
-    const uint64_t x = ws.Xs[g - 1];
-    if (ws.E[g] == x) return;
+    uint64_t x = ws.Xs[g - 1];
+    if (ws.Es[g] == x) return;
     const uint64_t len = st.lens[si];
-    const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
+    const uint64_t span = 1ull << st.span_log2;
     Reader r;
     init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
-    atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
-    if (rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf + threadIdx.x * kNew)) {
-        atomicAdd(&ws.flags[0], 1ull);  // exits changed: another round
-        atomicMin(&ws.flags[2], (unsigned long long)g);
+    uint64_t gg = g;
+    for (uint32_t k = 0;; ++k) {
+        const uint64_t seg_end = min(off + span, len);
+        atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
+        if (!rewalk<kAlgo, kBits>(x, gg, seg_end, len, r, wp, T, ws, nbuf + threadIdx.x * kNew)) break;
+        if (seg_end >= len) break;  // the stream's last segment: no successor
+        if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
+            atomicAdd(&ws.flags[0], 1ull);  // a successor needs another round
+            atomicMin(&ws.flags[2], (unsigned long long)gg);
+            break;
+        }
+        x = ws.X[gg];
+        ++gg;
+        off += span;
     }
 }
 
@@ -573,7 +604,7 @@ __device__ __forceinline__ void for_chunks(const uint8_t *base, uint64_t len, ui
 template <int kAlgo>
 __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, const WalkParams wp) {
     __shared__ uint64_t tab[768];
-    load_tabs(tab, wp.tabs);
+    if constexpr (kAlgo == 2 || kAlgo == 5) load_tabs(tab, wp.tabs);  // Ultra / Seq use no table
     const Tabs T{tab, tab + 256, tab + 512};
     const uint64_t g = blockIdx.x;
     uint32_t si;
@@ -581,11 +612,21 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     locate(st, g, si, off);
     const uint64_t len = st.lens[si];
     const uint8_t *base = st.ptrs[si];
-    const uint64_t w = 1ull << (st.span_log2 - 6);
-    const uint64_t p0 = off + threadIdx.x * w;
+    // Fine mode (Ultra, Leap, Seq): a lane evaluates one 64-position word at a
+    // time and the wave sweeps the segment 4 KiB per step, so each load
+    // instruction covers 4 KiB contiguous and each bitmap store is coalesced;
+    // the few window bytes before / after a word are re-read from cache.
+    // Rabin keeps one 1/64 range per lane (its 48-byte warm-up per range).
+    const uint64_t seg_bytes = 1ull << st.span_log2;
+    const bool fine = kAlgo != 2 && wp.bits_fine != 0;
+    const uint64_t w = fine ? 64 : seg_bytes >> 6;
+    const uint32_t reps = fine ? (uint32_t)(seg_bytes >> 12) : 1u;
+    for (uint32_t it = 0; it < reps; ++it) {
+    const uint64_t lidx = fine ? (uint64_t)it * 64 + threadIdx.x : threadIdx.x;
+    const uint64_t p0 = off + lidx * w;
     if (p0 >= len) return;
     const uint64_t p1 = min(p0 + w, len);
-    uint64_t *out = wp.bm + (g * wp.seg_words + threadIdx.x * (w >> 6)) * wp.nbm;
+    uint64_t *out = wp.bm + (g * wp.seg_words + lidx * (w >> 6)) * wp.nbm;
     if constexpr (kAlgo == 2) {
         // Rolling Rabin digest from 48 bytes before p0 (out bytes 0 until
         // 48 bytes are in): the digest after byte i is the fingerprint of the
@@ -691,6 +732,7 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             }
             prev = cur;
         });
+    }
     }
 }
 
@@ -807,6 +849,8 @@ hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkSt
 hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
     hipError_t e = hipMemcpyAsync(ws.Xs, ws.X, st.total_spans * 8, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(ws.Es, ws.E, st.total_spans * 8, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;
     return dispatch(1, st, wp, ws, s);
 }

@@ -35,6 +35,8 @@ struct WalkParams {
     uint64_t *bm;
     uint32_t nbm;             // 0 = byte mode; Rabin 1 (hit), Ultra 3 (mask_s, mask_l, 8-byte repeat), Leap 2
     uint32_t seg_words;       // 64-bit words per segment and bitmap (segment bytes / 64)
+    uint32_t bits_fine;       // bitmap pass: lane per 64-position word (Ultra, Leap, Seq)
+    uint32_t ahead;           // fix-up round: segments one lane may re-walk (1 = plain Jacobi)
 };
 
 struct WalkState {
@@ -43,6 +45,7 @@ struct WalkState {
     uint32_t *N;      // [S] chunk starts inside the segment
     uint64_t *list;   // [S * cap] those starts (stream offsets)
     uint64_t *Xs;     // [S] exits snapshot of a fix-up round
+    uint64_t *Es;     // [S] entries snapshot of a fix-up round
     uint64_t *P;      // [S + 1] exclusive prefix of N (chunk index of each segment)
     uint64_t *bsum;   // [blocks + 1] per-block sums of the prefix
     uint64_t *first;  // [n + 1] chunk index of each stream's first chunk
