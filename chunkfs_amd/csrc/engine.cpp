@@ -679,7 +679,10 @@ int Engine::init_walk(const uint32_t *seq) {
     // (tiny min), and segments >= 4 KiB.
     const uint32_t lmin = 63 - (uint32_t)__builtin_clzll((uint64_t)min_) + 12;
     if (seg_log2_ > lmin) seg_log2_ = lmin < 12 ? 12 : lmin;
-    uint64_t warm_mult = 8;
+    // SeqCDC chains (jumps skip most positions) merge more slowly: 16 avg
+    // (profiles/r02ag_walk_warm_sweep.log: 226 -> 241 GiB/s; the other rules
+    // gain nothing from a longer warm-up).
+    uint64_t warm_mult = algo_ == CDC_ALGO_SEQ ? 16 : 8;
     if (const char *w = std::getenv("CHUNKFS_AMD_WALK")) {
         unsigned a = 0, b = 0;
         if (std::sscanf(w, "%u,%u", &a, &b) == 2 && a >= 10 && a <= 30) {

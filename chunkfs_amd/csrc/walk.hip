@@ -279,6 +279,13 @@ __device__ uint64_t cut_ultra_bits(Reader &r, uint64_t s, uint64_t n, const Walk
                 i += 64;
                 continue;
             }
+            // The blocks before the first event neither repeat nor hit: skip
+            // to the event's block (lec is 0 after them, as block by block).
+            const uint32_t b = (uint32_t)__builtin_ctzll(e | m) >> 3;
+            if (b) {
+                lec = 0;
+                i += 8 * b;
+            }
         }
         if (r.bits(3, 2, s + i, 1)) {
             if (++lec >= CDC_ULTRA_LEST) return i + 8;
@@ -315,6 +322,23 @@ __device__ uint64_t cut_leap_bits(Reader &r, uint64_t s, uint64_t n, const WalkP
     return end;
 }
 
+// Index of the n-th (1-based) set bit of z, popc(z) >= n >= 1: a halving
+// search on popcounts (6 steps) instead of clearing n-1 bits one by one.
+__device__ __forceinline__ uint32_t select_bit(uint64_t z, uint32_t n) {
+    uint32_t pos = 0, c = (uint32_t)__popc((uint32_t)z);
+    if (c < n) { n -= c; z >>= 32; pos += 32; }
+    c = (uint32_t)__popc((uint32_t)z & 0xFFFFu);
+    if (c < n) { n -= c; z >>= 16; pos += 16; }
+    c = (uint32_t)__popc((uint32_t)z & 0xFFu);
+    if (c < n) { n -= c; z >>= 8; pos += 8; }
+    c = (uint32_t)__popc((uint32_t)z & 0xFu);
+    if (c < n) { n -= c; z >>= 4; pos += 4; }
+    c = (uint32_t)__popc((uint32_t)z & 0x3u);
+    if (c < n) { n -= c; z >>= 2; pos += 2; }
+    if (((uint32_t)z & 1u) < n) pos += 1;
+    return pos;
+}
+
 // SeqCDC over bitmap 0 (pair p in the mode's direction), up to 64 positions
 // per step: a = positions where a run of seq_len in-sequence pairs completes
 // (the run carried in from the previous step included), tB = the pair at which
@@ -334,11 +358,7 @@ __device__ uint64_t cut_seq_bits(Reader &r, uint64_t s, uint64_t n, const WalkPa
         a &= km;
         uint64_t z = ~y & km;
         const uint32_t need = wp.seq_trig - opp;
-        uint32_t tB = 64;
-        if ((uint32_t)__popcll(z) >= need) {
-            for (uint32_t q = 1; q < need; ++q) z &= z - 1;
-            tB = (uint32_t)__builtin_ctzll(z);
-        }
+        const uint32_t tB = (uint32_t)__popcll(z) >= need ? select_bit(z, need) : 64u;
         const uint32_t tA = a ? (uint32_t)__builtin_ctzll(a) : 64u;
         if (tA < tB) return i + tA + 1;
         if (tB < 64) {
