@@ -307,9 +307,20 @@ __device__ uint64_t cut_leap_bits(Reader &r, uint64_t s, uint64_t n, const WalkP
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
     uint64_t c = wp.min;
+    // The two primary words around the candidate stay in registers while the
+    // leaps (~21 positions each) move through them.
+    uint64_t kc = ~0ull, wa = 0, wb = 0;
     while (c <= end) {
-        const uint64_t z = ~r.bits(2, 0, s + c - CDC_LEAP_PRIMARY, CDC_LEAP_PRIMARY) &
-                           ((1ull << CDC_LEAP_PRIMARY) - 1);
+        const uint64_t p = s + c - CDC_LEAP_PRIMARY;
+        const uint64_t k = p >> 6;
+        if (k != kc) {
+            wa = r.word(k * 2);
+            wb = r.word(k * 2 + 2);
+            kc = k;
+        }
+        const uint32_t sh = (uint32_t)(p & 63);
+        const uint64_t v = sh ? (wa >> sh) | (wb << (64 - sh)) : wa;
+        const uint64_t z = ~v & ((1ull << CDC_LEAP_PRIMARY) - 1);
         if (z) {  // window k = 21 - j failed, j = the highest zero bit
             const uint32_t j = 63u - (uint32_t)__builtin_clzll(z);
             c += CDC_LEAP_WINDOWS - (CDC_LEAP_PRIMARY - 1 - j);
