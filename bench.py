@@ -68,6 +68,8 @@ def parse(argv=None):
     p.add_argument("--hash", action="store_true", help="also report the SHA-256 fingerprint rate (§8f row 2)")
     p.add_argument("--no-host-path", action="store_true",
                    help="skip the one-off host-buffer (PCIe-inclusive) rates")
+    p.add_argument("--config5-bytes", type=int, default=1 << 30,
+                   help="bytes of the bench stream the config-5 size sweep chunks")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU launcher test only
     # Multi-rank rehearsal on a box with fewer GPUs than ranks (tests only):
@@ -341,10 +343,13 @@ def algo_lines(args, eng, steps):
     return res
 
 
-def config5_lines(args, eng, nbytes=256 << 20, steps=2):
+def config5_lines(args, eng, steps=2):
     """Config 5's size sweep (BASELINE.json configs[4]) on one GPU: UltraCDC and
     LeapCDC (plus Rabin and Seq) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg
-    (SURVEY.md §8d), over a 256 MiB prefix of the bench stream; device GiB/s,
+    (SURVEY.md §8d), over the first --config5-bytes of the bench stream (default
+    the whole 1 GiB; config 5's share per GPU at 8 GPUs is 2 GiB, and the
+    segment-walk engine needs the bytes for lanes: at avg 64 KiB a segment is
+    256 KiB, so 256 MiB would be only 1024 lanes); device GiB/s,
     fraction of HBM peak, bit-exactness vs the oracle.  SuperCDC is not
     implemented (CDC_ENOTSUP)."""
     import numpy as np
@@ -352,7 +357,7 @@ def config5_lines(args, eng, nbytes=256 << 20, steps=2):
     import chunkfs_amd as cfa
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n = min(nbytes, eng.lens[0])
+    n = min(args.config5_bytes, eng.lens[0])
     buf = eng.bufs[0]
     host = buf[:n].cpu().numpy() if not args.no_parity else None
     res = {}

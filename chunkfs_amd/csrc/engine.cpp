@@ -671,10 +671,12 @@ int Engine::init_walk(const uint32_t *seq) {
     // Segments of 2^seg_log2 bytes (one lane each) and a warm-up of `warm`
     // bytes; CHUNKFS_AMD_WALK="seg_log2,warm_over_avg" overrides (experiments).
     // Defaults (tools/walk_bench.py sweeps on MI355X): segments of
-    // >= 4 avg and >= 32 KiB, a warm-up of 8 avg (a chain from an arbitrary
-    // start merges with the true one within a few content-defined cuts).
-    const uint32_t l2 = ceil_log2(avg_) + 2;
-    seg_log2_ = l2 < 15 ? 15 : l2;
+    // 32 KiB whatever the average (at avg 64 KiB, 32 KiB segments beat 256 KiB
+    // ones for every rule: more lanes, a shorter walk per lane and cheaper
+    // fix-up re-walks; profiles/r02ak_walk_avg64k_segments.log), a warm-up of
+    // 8 avg (a chain from an arbitrary start merges with the true one within a
+    // few content-defined cuts).
+    seg_log2_ = 15;
     // The per-segment start list holds segment/min + 2 entries: keep it <= ~4k
     // (tiny min), and segments >= 4 KiB.
     const uint32_t lmin = 63 - (uint32_t)__builtin_clzll((uint64_t)min_) + 12;
