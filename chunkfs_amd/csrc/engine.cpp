@@ -210,7 +210,10 @@ int Engine::ensure_host_staging(size_t n) {
     h_stage_ = nullptr;
     const size_t want = n + 64;
     // ptrs[W] lens[W] span_base[W] tails[W] | stats ++ first[n+1] (fixed: first[n+1])
-    HIP_TRY(hipHostMalloc(&h_stage_, (5 * want + 32) * sizeof(uint64_t), hipHostMallocCoherent));
+    // stream tables 4 n, device-written stats / flags ++ first[n+1] (n + 32),
+    // fix-up round flag blocks (4 x walk::kMaxFixRounds)
+    HIP_TRY(hipHostMalloc(&h_stage_, (5 * want + 32 + 4 * walk::kMaxFixRounds) * sizeof(uint64_t),
+                          hipHostMallocCoherent));
     h_stage_streams_ = want;
     return CDC_OK;
 }
@@ -748,7 +751,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     };
     const size_t oE = take(S * 8), oX = take(S * 8), oXs = take(S * 8), oEs = take(S * 8), oP = take((S + 1) * 8);
     const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
-    const size_t oF = take((N + 1) * 8), oG = take(4 * 8);
+    const size_t oF = take((N + 1) * 8), oG = take((4 + 4 * walk::kMaxFixRounds) * 8);
     const size_t oBM = take(S * (size_t)wp_.seg_words * wp_.nbm * 8);  // predicate bitmaps
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(wws_);
@@ -787,31 +790,52 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     HIP_TRY(walk::launch_walk(st, wp_, wst_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
     // Jacobi rounds: re-walk every segment whose entry is not its predecessor's
-    // exit, until none is (normally the first round finds none).
-    uint64_t rewalked = 0;
+    // exit, until none is.  Rounds are launched in groups without a host sync:
+    // round r counts into its own flag block (rf + 4 r) and returns at once on
+    // the device when round r-1 changed no exit (WalkState::gate), so the host
+    // waits once per group instead of once per round.
+    constexpr uint32_t kGroup = 4;
+    unsigned long long *rf = wst_.flags + 4;
+    uint64_t *h_rf = h + 5 * h_stage_streams_ + 32;
+    const uint32_t R = max_rounds_ < walk::kMaxFixRounds ? max_rounds_ : walk::kMaxFixRounds;
+    HIP_TRY(hipMemsetAsync(rf, 0, (size_t)R * 4 * 8, s));
+    HIP_TRY(hipMemset2DAsync(rf + 2, 32, 0xFF, 8, R, s));  // lowest segment whose exit changed
+    uint64_t rewalked = 0, round_errors = 0;
     bool settled = false;
-    for (uint32_t r = 0; r < max_rounds_ && !settled; ++r) {
-        // Plain Jacobi for the first ahead_after_ rounds, then run-ahead
-        // re-walks (walk.hip fix_kernel) so long non-merging stretches settle
-        // before the serial pass would be needed.
-        wp_.ahead = r < ahead_after_ ? 1u : ahead_max_;
-        HIP_TRY(hipMemsetAsync(wst_.flags, 0, 8, s));         // exits changed this round
-        HIP_TRY(hipMemsetAsync(wst_.flags + 2, 0xFF, 8, s));  // lowest segment whose exit changed
-        HIP_TRY(walk::launch_fix(st, wp_, wst_, s));
-        HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
+    uint32_t launched = 0;
+    while (launched < R && !settled) {
+        const uint32_t end = launched + kGroup < R ? launched + kGroup : R;
+        for (uint32_t r = launched; r < end; ++r) {
+            // Plain Jacobi for the first ahead_after_ rounds, then run-ahead
+            // re-walks (walk.hip fix_kernel) so long non-merging stretches
+            // settle before the serial pass would be needed.
+            wp_.ahead = r < ahead_after_ ? 1u : ahead_max_;
+            walk::WalkState ws = wst_;
+            ws.flags = rf + 4 * r;
+            ws.gate = r ? rf + 4 * (r - 1) : nullptr;
+            HIP_TRY(walk::launch_fix(st, wp_, ws, s));
+        }
+        launched = end;
+        HIP_TRY(hipMemcpyAsync(h_rf, rf, (size_t)launched * 4 * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        rewalked = h_flags[3];
-        settled = h_flags[0] == 0;
+        for (uint32_t r = 0; r < launched && !settled; ++r) settled = h_rf[4 * r] == 0;
+    }
+    for (uint32_t r = 0; r < launched; ++r) {
+        round_errors += h_rf[4 * r + 1];
+        rewalked += h_rf[4 * r + 3];
     }
     // Chains that never merge (periodic data): one exact in-order pass from
     // the lowest segment the last round changed.
-    if (!settled) HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
+    if (!settled) {
+        HIP_TRY(hipMemcpyAsync(wst_.flags + 2, rf + 4 * (R - 1) + 2, 8, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
+    }
     HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
     HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(ev_[2], s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (h_flags[1] != 0) {
+    if (h_flags[1] + round_errors != 0) {
         set_error("segment walk: chunk list or output bound exceeded (internal error)");
         return CDC_EDEVICE;
     }

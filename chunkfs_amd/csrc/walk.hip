@@ -522,6 +522,7 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
 template <int kAlgo, bool kBits>
 __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, const WalkParams wp,
                                                          const WalkState ws) {
+    if (ws.gate && *ws.gate == 0) return;  // the previous round settled everything
     __shared__ uint64_t tab[768];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWalkBlock * kSlot];
     __shared__ uint64_t nbuf[kWalkBlock * kNew];

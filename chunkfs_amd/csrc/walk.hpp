@@ -50,7 +50,12 @@ struct WalkState {
     uint64_t *bsum;   // [blocks + 1] per-block sums of the prefix
     uint64_t *first;  // [n + 1] chunk index of each stream's first chunk
     unsigned long long *flags;  // [4]: 0 exits changed this round, 1 errors, 2 lowest such segment, 3 re-walks
+    // Fix-up round only: the previous round's flag block; the round returns at
+    // once when that round changed no exit (null: always run).
+    const unsigned long long *gate;
 };
+
+constexpr uint32_t kMaxFixRounds = 16;  // flag blocks allocated after the main one
 
 constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
 
