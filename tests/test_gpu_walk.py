@@ -241,3 +241,34 @@ def test_many_small_streams_batch(algo):
     for i, n in enumerate(lens):
         ref = oracle.cdc(algo, host[offs[i]:offs[i] + n], *sizes)
         assert_same(got[first[i]:first[i + 1]], ref, f"{algo} stream {i} len {n}")
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("walk,ahead", [("12,1", "0,64"), ("12,1", "2,3"), ("13,2", "16,1")])
+def test_fixup_schedules_exact(algo, walk, ahead, monkeypatch):
+    """Fix-up round schedules the defaults rarely reach: tiny segments with a
+    1-avg warm-up make most entries wrong, then run-ahead from round 0
+    (ahead 64), a short run-ahead limit (3 segments), and plain Jacobi that
+    runs out of rounds into the serial pass.  Grouped rounds with device-side
+    gating are in every case.  Env is read at handle creation."""
+    import torch
+    import chunkfs_amd as c
+    from chunkfs_amd import _lib
+    monkeypatch.setenv("CHUNKFS_AMD_WALK", walk)
+    monkeypatch.setenv("CHUNKFS_AMD_AHEAD", ahead)
+    sizes = SIZES[algo][0]
+    cls = {"rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}.get(algo)
+    ch = cls(c.SizeParams(*sizes)) if cls else c.SeqChunker(0, c.SizeParams(*sizes))
+    n = (16 << 20) + 4321
+    b = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    _lib.check(_lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, 17, None))
+    cap = ch.batch_max_chunks([n])
+    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    first = ch.chunk_batch_device([b.data_ptr()], [n], out.data_ptr(), cap)
+    got = out[:first[1]].cpu().numpy().astype(np.uint64)
+    assert_same(got, oracle.cdc(algo, b.cpu().numpy(), *sizes), f"{algo} walk={walk} ahead={ahead}")
+    assert ch.last_timing()["fixup_iterations"] > 0  # the fix-up rounds did run
+    data = make_input("periodic", 600000, 61)
+    assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} periodic walk={walk} ahead={ahead}")
+    ch.close()
