@@ -42,14 +42,16 @@ __device__ __forceinline__ void locate(const StreamTable &st, uint64_t g, uint32
 // pays one memory latency per >= kWin - kBack - 16 bytes of progress instead
 // of one per divergent 16-byte miss.  Bytes past the stream end read as 0 and
 // are never loaded.
-constexpr uint32_t kWin = 1024;               // window bytes per lane
+constexpr uint32_t kWin = 512;                // window bytes per lane
 constexpr uint32_t kBack = 64;                // bytes kept behind the position at a refill
 constexpr uint32_t kSlot = kWin + 16;         // LDS stride per lane (bank spread)
 
 // Refill of one lane's window (out of line: one copy per kernel, called from
 // every read site); returns the new window start.  The window is loaded in
 // batches of 16 global_load_dwordx4 with the next batch in flight while the
-// previous one is written to LDS (64 + 64 VGPRs, no spills at kWin = 1 KiB).
+// previous one is written to LDS (64 + 64 VGPRs, no spills).  512 B windows
+// (39 KiB per one-wave walk block) keep 4 walk waves per CU: 1 KiB windows
+// held 2 and ran inputs above 1 GiB in batches (profiles/r02at, r02au).
 constexpr uint32_t kBatch = 16;
 
 __device__ __forceinline__ uint4 load_piece(const uint8_t *base, uint64_t len, uint64_t a) {
