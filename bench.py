@@ -6,12 +6,16 @@ resolve -> Chunk{offset,length} list in HBM) over the rank's synthetic input,
 which is already resident in HBM when the timed region starts.
 
 Workloads:
-  * N = 1 (default `--workload stream`): BASELINE configs[1] / config 2 --
-    one 1 GiB stream of splitmix64(seed=1) bytes, FastCDC 4/8/16 KiB.
-  * N > 1 (default `--workload batch`): config 4 -- 1024 independent 64 MiB
-    streams (stream i: seed 1000+i) split into contiguous blocks across the
-    ranks, strong scaling, no data-path collective (chunkfs_amd/sharding.py).
-    `--workload stream` at N > 1 gives every rank its own 1 GiB stream (weak).
+  * `value` (default `--workload stream`, every N): BASELINE configs[1] /
+    config 2 -- one 1 GiB stream of splitmix64(seed=1+rank) bytes per GPU,
+    FastCDC 4/8/16 KiB, weak scaling: the per-GPU work is the same at every N,
+    so the driver's N=1 line is the matching denominator of its 1->8 curve.
+  * `config4` sub-object (every N, unless --no-config4): config 4 -- 1024
+    independent 64 MiB streams (stream i: seed 1000+i) split into contiguous
+    blocks across the ranks, strong scaling, no data-path collective
+    (chunkfs_amd/sharding.py).  At N > 1 rank 0 also times the whole 1024-
+    stream batch alone in the same run, the N=1 denominator of that line's
+    strong-scaling efficiency.  `--workload batch` makes config 4 `value`.
 
 Launch: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the
 environment starts `torch.distributed.run` with N ranks as a CHILD process
@@ -47,12 +51,15 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["stream", "batch"], default=None,
-                   help="default: stream at N=1, batch (config 4) at N>1")
+    p.add_argument("--workload", choices=["stream", "batch"], default="stream",
+                   help="what `value` measures: stream = config 2 per GPU (weak), batch = config 4 (strong)")
     p.add_argument("--stream-bytes", type=int, default=1 << 30)
     p.add_argument("--batch-streams", type=int, default=1024,
                    help="config 4: total streams, split across ranks (strong scaling)")
     p.add_argument("--batch-stream-bytes", type=int, default=64 << 20)
+    p.add_argument("--no-config4", action="store_true",
+                   help="skip the config-4 (1024 x 64 MiB, strong scaling) sub-object")
+    p.add_argument("--config4-steps", type=int, default=5)
     p.add_argument("--min", type=int, default=4096)
     p.add_argument("--avg", type=int, default=8192)
     p.add_argument("--max", type=int, default=16384)
@@ -78,10 +85,7 @@ def parse(argv=None):
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
     p.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--rank-parity", action="store_true", help=argparse.SUPPRESS)
-    a = p.parse_args(argv)
-    if a.workload is None:
-        a.workload = "stream" if a.gpus == 1 else "batch"
-    return a
+    return p.parse_args(argv)
 
 
 # ---------------------------------------------------------------------------
@@ -111,6 +115,14 @@ def launch_ranks(args, argv):
 # tests/test_bench_launcher.py exercise the launcher and the reductions with
 # gloo on a machine without a GPU.  The stub is never a product path.
 
+class Work:
+    """One workload resident on the rank's device: streams, output, capacity."""
+
+    def __init__(self, lens):
+        self.lens = list(lens)
+        self.bufs, self.out = [], None
+
+
 class DeviceEngine:
     def __init__(self, args, local):
         import torch
@@ -121,25 +133,23 @@ class DeviceEngine:
         self.local = local
         self.ch = cfa.FastChunker(cfa.SizeParams(args.min, args.avg, args.max), device=local)
 
-    def fill(self, lens, seeds):
+    def prepare(self, lens, seeds):
+        import numpy as np
         torch = self.torch
-        self.bufs = []
+        w = Work(lens)
         for n, s in zip(lens, seeds):
             b = torch.empty(max(n, 16), dtype=torch.uint8, device=self.dev)
             self._lib.check(self._lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, s, None))
-            self.bufs.append(b)
-        self.lens = list(lens)
-        self.ptrs = [b.data_ptr() for b in self.bufs]
-        import numpy as np
-        self.ptrs_a = np.array(self.ptrs, dtype=np.uint64)  # converted once, not per step
-        self.lens_a = np.array(self.lens, dtype=np.uint64)
-        self.cap = self.ch.batch_max_chunks(self.lens)
-        self.out = torch.empty((max(self.cap, 1), 2), dtype=torch.int64, device=self.dev)
-        self.out_ptr = self.out.data_ptr()
+            w.bufs.append(b)
+        w.ptrs_a = np.array([b.data_ptr() for b in w.bufs], dtype=np.uint64)  # converted once, not per step
+        w.lens_a = np.array(w.lens, dtype=np.uint64)
+        w.cap = self.ch.batch_max_chunks(w.lens)
+        w.out = torch.empty((max(w.cap, 1), 2), dtype=torch.int64, device=self.dev)
         torch.cuda.synchronize()
+        return w
 
-    def step(self):
-        return self.ch.chunk_batch_device(self.ptrs_a, self.lens_a, self.out_ptr, self.cap)
+    def step(self, w):
+        return self.ch.chunk_batch_device(w.ptrs_a, w.lens_a, w.out.data_ptr(), w.cap)
 
     def timing(self):
         return self.ch.last_timing()
@@ -155,12 +165,12 @@ class StubEngine:
         self.dev = torch.device("cpu")
         self.cs = args.avg
 
-    def fill(self, lens, seeds):
-        self.lens = list(lens)
+    def prepare(self, lens, seeds):
+        return Work(lens)
 
-    def step(self):
+    def step(self, w):
         first = [0]
-        for n in self.lens:
+        for n in w.lens:
             first.append(first[-1] + -(-n // self.cs))
         return first
 
@@ -169,6 +179,76 @@ class StubEngine:
 
     def sync(self):
         pass
+
+
+def timed_steps(eng, w, steps, warmup, world, red_dev):
+    """W untimed + K timed steps of workload w, bracketed by a barrier and a
+    device sync on both sides; returns (max-over-ranks seconds, last first[],
+    per-step engine timings)."""
+    import torch.distributed as dist
+    from chunkfs_amd import sharding
+    first = None
+    for _ in range(warmup):
+        first = eng.step(w)
+    if world > 1:
+        dist.barrier()
+    eng.sync()
+    tims = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        first = eng.step(w)
+        tims.append(eng.timing())
+    eng.sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        el = sharding.max_over_ranks(el, red_dev)
+    return el, first, tims
+
+
+def config4_leg(args, eng, rank, world, red_dev):
+    """Config 4 (BASELINE configs[3]): 1024 x 64 MiB streams split across the
+    ranks (strong scaling, no data-path collective); at N > 1 rank 0 also times
+    the whole batch alone in this run (the N=1 denominator)."""
+    import torch.distributed as dist
+    from chunkfs_amd import sharding
+    shard = sharding.batch_shard(rank, world, args.batch_streams, args.batch_stream_bytes)
+    w = eng.prepare(shard.lens, shard.seeds)
+    steps = max(1, args.config4_steps)
+    el, first, tims = timed_steps(eng, w, steps, 2, world, red_dev)
+    total = sharding.sum_over_ranks(sum(shard.lens), red_dev) * steps
+    scan = sum(t["scan_ms"] for t in tims) / len(tims)
+    out = {"workload": f"config4: {args.batch_streams} x {args.batch_stream_bytes} B streams split across "
+                       f"{world} GPU(s)", "scaling": "strong", "steps": steps,
+           "value": sharding.aggregate_gibps(total, el), "unit": "GiB/s", "ms_per_step": el / steps * 1e3,
+           "streams_per_gpu": len(shard.lens), "bytes_per_gpu": sum(shard.lens),
+           "chunks_total": sharding.sum_over_ranks(int(first[-1]) if first is not None else 0, red_dev),
+           "scan_ms": scan,
+           "scan_frac_of_hbm": (sum(shard.lens) / (scan * 1e-3) / 1e9 / HBM_PEAK_GBS) if scan > 0 else None}
+    if not args.no_parity and not args.stub and rank == 0 and len(shard.lens):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import numpy as np
+        import oracle
+        ok = True
+        for i in range(min(len(shard.lens), 2)):
+            got = w.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
+            ref = oracle.fastcdc(w.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
+            ok &= bool(got.shape == ref.shape and (got == ref).all())
+        out["parity_vs_oracle"] = ok
+    del w
+    if world > 1:
+        n1 = None
+        if rank == 0:
+            whole = sharding.batch_shard(0, 1, args.batch_streams, args.batch_stream_bytes)
+            w1 = eng.prepare(whole.lens, whole.seeds)
+            el1, _, _ = timed_steps(eng, w1, steps, 2, 1, None)
+            n1 = sum(whole.lens) * steps / el1 / (1 << 30)
+            del w1
+        dist.barrier()
+        if rank == 0:
+            out["n1_value_rank0_alone"] = n1
+            out["strong_scaling_efficiency"] = out["value"] / (world * n1)
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -243,7 +323,7 @@ def traffic_for_build(path, bytes_rank):
     return None, None
 
 
-def sweep_lines(args, eng, steps):
+def sweep_lines(args, eng, w, steps):
     """Extra single-GPU lines: avg 4 KiB and 16 KiB (min = avg/2, max = 2*avg)
     on the same 1 GiB stream, and 1 GiB of low-entropy data (zeros; a 61-byte
     period) at 4/8/16 KiB, each with an oracle parity check after timing."""
@@ -252,8 +332,8 @@ def sweep_lines(args, eng, steps):
     import chunkfs_amd as cfa
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n = eng.lens[0]
-    base = eng.bufs[0]
+    n = w.lens[0]
+    base = w.bufs[0]
     period = torch.from_numpy(oracle.splitmix64_bytes(61, 7)).to(eng.dev)
     inputs = {
         "splitmix64": base,
@@ -293,7 +373,7 @@ def sweep_lines(args, eng, steps):
     return res
 
 
-def algo_lines(args, eng, steps):
+def algo_lines(args, eng, w, steps):
     """Rabin / UltraCDC / LeapCDC / SeqCDC (segment-walk engine) over the same
     1 GiB stream at the bench sizes: device GiB/s, the walk / fix-up split,
     bit-exactness against the oracle on the whole stream, and the oracle's
@@ -303,8 +383,8 @@ def algo_lines(args, eng, steps):
     import chunkfs_amd as cfa
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n = eng.lens[0]
-    buf = eng.bufs[0]
+    n = w.lens[0]
+    buf = w.bufs[0]
     sizes = cfa.SizeParams(args.min, args.avg, args.max)
     host = buf[:n].cpu().numpy() if not args.no_parity else None
     res = {}
@@ -343,7 +423,7 @@ def algo_lines(args, eng, steps):
     return res
 
 
-def config5_lines(args, eng, steps=2):
+def config5_lines(args, eng, w, steps=2):
     """Config 5's size sweep (BASELINE.json configs[4]) on one GPU: UltraCDC and
     LeapCDC (plus Rabin and Seq) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg
     (SURVEY.md §8d), over the first --config5-bytes of the bench stream (default
@@ -357,8 +437,8 @@ def config5_lines(args, eng, steps=2):
     import chunkfs_amd as cfa
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    n = min(args.config5_bytes, eng.lens[0])
-    buf = eng.bufs[0]
+    n = min(args.config5_bytes, w.lens[0])
+    buf = w.bufs[0]
     host = buf[:n].cpu().numpy() if not args.no_parity else None
     res = {}
     for avg in (2048, 8192, 65536):
@@ -388,41 +468,10 @@ def config5_lines(args, eng, steps=2):
     return {"bytes": int(n), "lines": res}
 
 
-def versioned_archive(base_bytes, versions, seed=3):
-    """SURVEY.md §8d config 3's offline substitute for the gcc tarball: a seeded
-    random base blob and `versions - 1` successive copies, each with seeded
-    overwrites, inserts and deletes totalling ~1 % of its bytes."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    rng = np.random.default_rng(seed)
-    out = [oracle.splitmix64_bytes(base_bytes, seed)]
-    for _ in range(versions - 1):
-        v = out[-1]
-        budget = v.size // 100
-        parts, pos = [], 0
-        for p in np.sort(rng.choice(v.size - 8192, size=max(1, budget // 2048), replace=False)):
-            if p < pos:
-                continue
-            parts.append(v[pos:p])
-            k = int(rng.integers(64, 4096))
-            op = int(rng.integers(0, 3))
-            if op == 0:    # overwrite k bytes
-                parts.append(rng.integers(0, 256, k, dtype=np.uint8))
-                pos = p + k
-            elif op == 1:  # insert k bytes
-                parts.append(rng.integers(0, 256, k, dtype=np.uint8))
-                pos = p
-            else:          # delete k bytes
-                pos = p + k
-        parts.append(v[pos:])
-        out.append(np.ascontiguousarray(np.concatenate(parts)))
-    return out
-
-
-def config3_line(args, local, base_bytes=64 << 20, versions=8):
+def config3_line(args, local, base_bytes=256 << 20, versions=16):
     """Config 3 (BASELINE.json configs[2]): RabinChunker 2/4/8 KiB over a
-    versioned archive; every version is one file write (a fresh StorageWriter,
+    versioned archive at SURVEY.md §8d's size (256 MiB base + 15 edited
+    copies, ~4 GiB; chunkfs_amd.synthetic); every version is one file write (a fresh StorageWriter,
     storage.rs:79).  GPU: chunk -> SHA-256 per chunk -> dedup index, all
     device-resident; dedup ratio = size_written / unique bytes (storage.rs:
     203-205).  CPU: the oracle's chunks, hashlib SHA-256 and a dict (first
@@ -433,6 +482,7 @@ def config3_line(args, local, base_bytes=64 << 20, versions=8):
     import chunkfs_amd as cfa
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    from chunkfs_amd.synthetic import versioned_archive
     sizes = (2048, 4096, 8192)
     files = versioned_archive(base_bytes, versions)
     total = sum(f.size for f in files)
@@ -483,14 +533,14 @@ def config3_line(args, local, base_bytes=64 << 20, versions=8):
             "cpu_definition": "oracle Rabin (C) + hashlib SHA-256 + dict, single thread"}
 
 
-def host_path_leg(eng):
+def host_path_leg(eng, w):
     """PCIe-inclusive rates of the host boundary, recorded beside `value`,
     never as it: cdc_chunk_data on a 1 GiB host buffer, and the
     reference harness's own measure -- the StorageWriter loop over 1 MiB
     segments, bytes / summed chunk_data seconds (src/bench/mod.rs:93-140,
     src/system/storage.rs:314-316)."""
     import chunkfs_amd as cfa
-    hb = eng.bufs[0][:eng.lens[0]].cpu().numpy()
+    hb = w.bufs[0][:w.lens[0]].cpu().numpy()
     ch = eng.ch
     ch.chunk_array(hb)
     reps, t_h = 3, time.perf_counter()
@@ -549,33 +599,13 @@ def main(argv=None):
         shard = sharding.stream_shard(rank, world, args.stream_bytes)
     else:
         shard = sharding.batch_shard(rank, world, args.batch_streams, args.batch_stream_bytes)
-    eng.fill(shard.lens, shard.seeds)
-
-    for _ in range(args.warmup):
-        first = eng.step()
-
-    if world > 1:
-        dist.barrier()
-    eng.sync()
-    scan_ms, total_ms, resolve_ms, rewalked, fallback = [], [], [], [], []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        first = eng.step()
-        t = eng.timing()
-        scan_ms.append(t["scan_ms"])
-        total_ms.append(t["total_ms"])
-        resolve_ms.append(t["resolve_ms"])
-        rewalked.append(t["fixup_iterations"])
-        fallback.append(t.get("walk_fallback_steps", 0))
-    eng.sync()
-    if world > 1:
-        dist.barrier()
-    elapsed = sharding.max_over_ranks(time.perf_counter() - t0, red_dev)
+    w = eng.prepare(shard.lens, shard.seeds)
+    elapsed, first, tims = timed_steps(eng, w, args.steps, args.warmup, world, red_dev)
 
     bytes_rank = sum(shard.lens)
     total_bytes = sharding.sum_over_ranks(bytes_rank, red_dev) * args.steps
     value = sharding.aggregate_gibps(total_bytes, elapsed)
-    scan_avg_ms = sum(scan_ms) / len(scan_ms)
+    scan_avg_ms = sum(t["scan_ms"] for t in tims) / len(tims)
     nchunks = int(first[-1])
     total_chunks = sharding.sum_over_ranks(nchunks, red_dev)
     ms_per_step = elapsed / args.steps * 1e3
@@ -589,31 +619,31 @@ def main(argv=None):
             dig = torch.empty((max(n0, 1), 32), dtype=torch.uint8, device=dev)
             hms = []
             for _ in range(3):
-                eng.ch.sha256_chunks_device(eng.bufs[0].data_ptr(), eng.out.data_ptr(), n0, dig.data_ptr())
+                eng.ch.sha256_chunks_device(w.bufs[0].data_ptr(), w.out.data_ptr(), n0, dig.data_ptr())
                 hms.append(eng.ch.last_timing()["hash_ms"])
             hm = sorted(hms)[1]
             extras["fingerprint"] = {"algo": "SHA-256 per chunk (Sha256Hasher)", "chunks": n0, "kernel_ms": hm,
                                      "GiBps": shard.lens[0] / (hm * 1e-3) / (1 << 30)}
         if not args.no_host_path:
-            extras["host_path"] = host_path_leg(eng)
+            extras["host_path"] = host_path_leg(eng, w)
         if not args.no_parity:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             checked = []
             for i in range(min(len(shard.lens), 4)):
-                got = eng.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
-                ref = oracle.fastcdc(eng.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
+                got = w.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
+                ref = oracle.fastcdc(w.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
                 checked.append(bool(got.shape == ref.shape and (got == ref).all()))
             extras["parity_vs_oracle"] = all(checked)
             extras["parity_streams_checked"] = len(checked)
         if not args.no_sweep and args.workload == "stream":
-            extras["sweep"] = sweep_lines(args, eng, max(5, args.steps // 2))
+            extras["sweep"] = sweep_lines(args, eng, w, max(5, args.steps // 2))
         if not args.no_algos and args.workload == "stream":
-            extras["other_chunkers"] = algo_lines(args, eng, 3)
+            extras["other_chunkers"] = algo_lines(args, eng, w, 3)
             extras["config3"] = config3_line(args, local)
-            extras["config5_1gpu"] = config5_lines(args, eng)
+            extras["config5_1gpu"] = config5_lines(args, eng, w)
         if args.cpu_seconds > 0:
-            extras["cpu_baseline"] = cpu_baseline_leg(args, eng.bufs[0][:shard.lens[0]].cpu().numpy())
+            extras["cpu_baseline"] = cpu_baseline_leg(args, w.bufs[0][:shard.lens[0]].cpu().numpy())
             fw = extras.get("host_path", {}).get("fs_write_1MiB_segments")
             if fw:
                 fw["x_cpu_single_thread"] = fw["GiBps"] / extras["cpu_baseline"]["value"]
@@ -623,10 +653,16 @@ def main(argv=None):
         import oracle
         ok = 1
         for i in range(min(len(shard.lens), 2)):
-            got = eng.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
-            ref = oracle.fastcdc(eng.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
+            got = w.out[int(first[i]):int(first[i + 1])].cpu().numpy().view(np.uint64)
+            ref = oracle.fastcdc(w.bufs[i][:shard.lens[i]].cpu().numpy(), args.min, args.avg, args.max)
             ok &= int(got.shape == ref.shape and bool((got == ref).all()))
         extras["parity_all_ranks"] = bool(sharding.min_over_ranks(ok, red_dev)) if world > 1 else bool(ok)
+
+    if not args.no_config4 and args.workload == "stream":
+        del w
+        c4 = config4_leg(args, eng, rank, world, red_dev)
+        if rank == 0:
+            extras["config4"] = c4
 
     traffic, traffic_src = traffic_for_build(args.traffic_json, bytes_rank)
     if rank == 0:
@@ -661,9 +697,10 @@ def main(argv=None):
                                "definition": "per-GPU input bytes / wall ms_per_step"},
             },
             "cpu_baseline": extras.pop("cpu_baseline", None),
-            "phase_ms": {"scan": scan_avg_ms, "total_device": sum(total_ms) / len(total_ms),
-                         "resolve": sum(resolve_ms) / len(resolve_ms), "rewalked_spans": max(rewalked),
-                         "walk_fallback_steps": max(fallback)},
+            "phase_ms": {"scan": scan_avg_ms, "total_device": sum(t["total_ms"] for t in tims) / len(tims),
+                         "resolve": sum(t["resolve_ms"] for t in tims) / len(tims),
+                         "rewalked_spans": max(t["fixup_iterations"] for t in tims),
+                         "walk_fallback_steps": max(t.get("walk_fallback_steps", 0) for t in tims)},
         }
         line.update(extras)
         if args.stub:

@@ -194,7 +194,7 @@ class Chunker:
 
     def last_timing(self):
         t = cdc_timing_t()
-        check(lib().cdc_last_timing(self._h, ctypes.byref(t)))
+        check(lib().cdc_last_timing(self._h, ctypes.byref(t), ctypes.sizeof(t)))
         return {f: getattr(t, f) for f, _ in cdc_timing_t._fields_}
 
     def set_gear(self, gear):
@@ -257,8 +257,11 @@ class UltraChunker(_SizedChunker):
 
 
 class LeapChunker(_SizedChunker):
-    """Leap-based CDC (src/chunkers/leap.rs:30-44): 24 eligible windows before a
-    cut, leaping past a failing window."""
+    """Leap-shaped CDC for LeapChunker (src/chunkers/leap.rs:30-44): 24 eligible
+    windows before a cut, leaping past a failing window, as in the Leap-based
+    CDC paper.  The window eligibility function is a STAND-IN (a seeded table
+    hash against a threshold, include/chunkfs_amd_cdc_params.h), not the
+    published one the crate builds from random draws: parity unpinned."""
     _algo, _name = "leap", "LeapChunker"
 
 

@@ -25,7 +25,7 @@ EXPORTS = [
     "cdc_fs_write", "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
     "cdc_index_create", "cdc_index_destroy", "cdc_index_clear", "cdc_index_insert_device",
     "cdc_index_stats",
-    "cdc_fill_splitmix64_device", "cdc_version",
+    "cdc_fill_splitmix64_device", "cdc_version", "cdc_abi_version",
 ]
 # include/chunkfs_amd_debug.h (diagnostics, not part of the drop-in boundary)
 DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy"]
@@ -113,7 +113,7 @@ def lib():
     L.cdc_chunk_batch_device.restype = ctypes.c_int64
     L.cdc_batch_max_chunks.argtypes = [P, sz, u64p]
     L.cdc_batch_max_chunks.restype = sz
-    L.cdc_last_timing.argtypes = [P, ctypes.POINTER(cdc_timing_t)]
+    L.cdc_last_timing.argtypes = [P, ctypes.POINTER(cdc_timing_t), sz]
     L.cdc_last_timing.restype = ctypes.c_int
     L.cdc_fs_write.argtypes = [P, P, sz, sz, u64p, sz, ctypes.POINTER(ctypes.c_double)]
     L.cdc_fs_write.restype = ctypes.c_int64
@@ -141,6 +141,8 @@ def lib():
     L.cdc_debug_copy.restype = ctypes.c_int64
     L.cdc_version.argtypes = []
     L.cdc_version.restype = ctypes.c_char_p
+    L.cdc_abi_version.argtypes = []
+    L.cdc_abi_version.restype = ctypes.c_uint32
     del u8p
     _lib = L
     return L

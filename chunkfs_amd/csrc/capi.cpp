@@ -1,4 +1,5 @@
 // capi.cpp -- extern "C" entry points of libchunkfs_amd.so (include/chunkfs_amd.h).
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -83,9 +84,10 @@ size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n, const uint64_t *len
     return (h && lens) ? h->engine->batch_max_chunks(n, lens) : 0;
 }
 
-int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t) {
+int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size) {
     if (!h || !t) return (int)bad_handle();
-    *t = h->engine->timing();
+    const cdc_timing_t &src = h->engine->timing();
+    std::memcpy(t, &src, t_size < sizeof src ? t_size : sizeof src);
     return CDC_OK;
 }
 
@@ -150,6 +152,8 @@ int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes) {
     return h->engine->debug_copy(what, out, max_bytes);
 }
 
-const char *cdc_version(void) { return "chunkfs_amd 0.1 gfx950 abi 1"; }
+const char *cdc_version(void) { return "chunkfs_amd 0.3 gfx950 abi 2"; }
+
+uint32_t cdc_abi_version(void) { return CHUNKFS_AMD_ABI_VERSION; }
 
 }  // extern "C"

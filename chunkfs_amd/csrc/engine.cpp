@@ -8,6 +8,7 @@
 // leave HBM.
 #include "engine.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -290,7 +291,9 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
             set_error("NULL stream pointer with non-zero length");
             return CDC_EINVAL;
         }
-        if (lens[i] && algo_ == CDC_ALGO_FASTCDC && (reinterpret_cast<uintptr_t>(d_streams[i]) & 15)) {
+        // Every content-defined kernel reads streams with 16-byte vector loads
+        // (FastCDC scan, walk-engine bitmap pass and LDS windows).
+        if (lens[i] && algo_ != CDC_ALGO_FIXED && (reinterpret_cast<uintptr_t>(d_streams[i]) & 15)) {
             set_error("device stream pointers must be 16-byte aligned");
             return CDC_EINVAL;
         }
@@ -379,13 +382,16 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     HIP_TRY(hipEventRecord(ev_[2], s));
     // The resolve's last block writes the done word into coherent pinned
     // memory after a system-scope fence: spin on it (wakes faster than a
-    // blocking stream sync), bounded, then the stream sync confirms.
+    // blocking stream sync) for about the batch's expected device time
+    // (bytes at ~2 TB/s, 0.1-5 ms), pausing between polls, then the stream
+    // sync confirms.  Long batches or a busy caller stream fall through to
+    // the blocking sync instead of burning a core.
     {
         const volatile uint64_t *done = h_misc + p3::kStatDone;
+        const auto budget = std::chrono::microseconds(
+            std::min<uint64_t>(5000, std::max<uint64_t>(100, timing_.bytes / 2000000)));
         const auto t_spin = std::chrono::steady_clock::now();
-        while (*done == ~0ull &&
-               std::chrono::steady_clock::now() - t_spin < std::chrono::milliseconds(200)) {
-        }
+        while (*done == ~0ull && std::chrono::steady_clock::now() - t_spin < budget) __builtin_ia32_pause();
     }
     HIP_TRY(hipStreamSynchronize(s));
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {

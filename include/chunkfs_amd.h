@@ -25,7 +25,9 @@
 extern "C" {
 #endif
 
-#define CHUNKFS_AMD_ABI_VERSION 1
+/* 2: cdc_last_timing takes the caller's sizeof(cdc_timing_t) (the struct
+ *    may grow; fields are only ever appended); cdc_abi_version(). */
+#define CHUNKFS_AMD_ABI_VERSION 2
 
 /* Chunk{offset,length} -- reference src/lib.rs:43-47 (usize fields; u64 here). */
 typedef struct cdc_chunk {
@@ -40,7 +42,8 @@ typedef enum cdc_algo {
     CDC_ALGO_RABIN = 2,   /* RabinChunker (src/chunkers/rabin.rs)    -- parity unpinned */
     CDC_ALGO_SUPER = 3,   /* SuperChunker (src/chunkers/supercdc.rs) -- CDC_ENOTSUP */
     CDC_ALGO_ULTRA = 4,   /* UltraChunker (src/chunkers/ultra.rs)    -- parity unpinned */
-    CDC_ALGO_LEAP = 5,    /* LeapChunker  (src/chunkers/leap.rs)     -- parity unpinned */
+    CDC_ALGO_LEAP = 5,    /* LeapChunker  (src/chunkers/leap.rs)     -- leap structure of the paper,
+                             stand-in eligibility function (chunkfs_amd_cdc_params.h) */
     CDC_ALGO_SEQ = 6      /* SeqChunker   (src/chunkers/seq.rs)      -- parity unpinned */
 } cdc_algo_t;
 
@@ -59,8 +62,10 @@ typedef struct cdc_handle cdc_handle_t;
  *   CDC_ALGO_RABIN / _ULTRA / _LEAP: RabinChunker / UltraChunker / LeapChunker
  *                     ::new(SizeParams{min,avg,max}) (rabin.rs:13-20,
  *                     ultra.rs:12-16, leap.rs:12-16).  The reference's crate
- *                     (cdc-chunkers 0.1.3) is absent: the cut rules restate the
- *                     published algorithms, parity unpinned.
+ *                     (cdc-chunkers 0.1.3) is absent: Rabin / Ultra restate the
+ *                     published algorithms, parity unpinned; Leap
+ *                     keeps the paper's leap structure with a STAND-IN window
+ *                     eligibility function (not the published one).
  *                     Sizes: 0 < min <= avg <= max; Ultra min >= 8, Leap min >= 32.
  *   CDC_ALGO_SEQ:     SeqChunker with OperationMode::Increasing and the default
  *                     Config (cdc_create_seq for the full constructor).
@@ -149,7 +154,10 @@ typedef struct cdc_timing {
     uint64_t walk_fallback_steps; /* chain-walk steps without a precomputed record link */
 } cdc_timing_t;
 
-int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t);
+/* Copies min(t_size, sizeof(cdc_timing_t)) bytes: pass sizeof(cdc_timing_t)
+ * of the header the caller was built with, so an older (shorter) struct is
+ * never overrun when fields are appended in a later version. */
+int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size);
 
 /* ---- Write path mirror --------------------------------
  * ChunkStorage::write (storage.rs:78-103) + StorageWriter::{write,flush}
@@ -216,8 +224,11 @@ int cdc_index_stats(const cdc_index_t *ix, cdc_index_stats_t *out);
 int cdc_fill_splitmix64_device(uint8_t *d_buf, size_t len, uint64_t seed,
                                void *hip_stream);
 
-/* Engine build info, e.g. "chunkfs_amd 0.1 gfx950 abi 1". */
+/* Engine build info, e.g. "chunkfs_amd 0.3 gfx950 abi 2". */
 const char *cdc_version(void);
+
+/* CHUNKFS_AMD_ABI_VERSION of the loaded library (compare with the header's). */
+uint32_t cdc_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -30,9 +30,17 @@
 /* LeapCDC: a cut after position p needs 24 consecutive eligible windows
  * ending at p, p-1, ..., p-23 (22 primary, then 2 secondary), each window
  * CDC_LEAP_WSIZE bytes; a failing window at distance k leaps the candidate
- * forward by 24 - k.  The eligibility function is a table hash of the window
- * (CDC_LEAP_SEED) compared with a threshold chosen so that 24 successes have
- * probability ~2^-bits, bits = round(log2(avg - min)). */
+ * forward by 24 - k.  That leap structure follows the Leap-based CDC paper.
+ *
+ * STAND-IN ELIGIBILITY FUNCTION.  The window test below -- a table hash of
+ * the window (CDC_LEAP_SEED) compared with a threshold chosen so that 24
+ * successes have probability ~2^-bits, bits = round(log2(avg - min)) -- is
+ * this build's own placeholder, NOT the published Leap-based CDC eligibility
+ * function (which cdc-chunkers 0.1.3 builds from random draws: it depends on
+ * rand 0.8.5 / rand_distr 0.4.3, Cargo.lock:143-151, absent here).  The
+ * chunker is therefore "Leap-shaped", not LeapCDC.  Pinning means replacing
+ * the eligibility function (bits_kernel's primary / secondary predicates and
+ * oracle cut_leap); every constant it uses is one named value here. */
 #define CDC_LEAP_WINDOWS 24u
 #define CDC_LEAP_PRIMARY 22u
 #define CDC_LEAP_WSIZE 5u

@@ -342,7 +342,9 @@ static void leap_table(uint64_t e[256])
 
 static inline uint64_t rotl64(uint64_t x, unsigned r) { return r ? (x << r) | (x >> (64 - r)) : x; }
 
-/* Window hash of the CDC_LEAP_WSIZE bytes ending at src[p]. */
+/* Window hash of the CDC_LEAP_WSIZE bytes ending at src[p].  STAND-IN
+ * eligibility function (include/chunkfs_amd_cdc_params.h): not the published
+ * Leap-based CDC one; only cut_leap's leap structure follows the paper. */
 static inline uint64_t leap_hash(const uint8_t *src, uint64_t p, const uint64_t *e)
 {
     uint64_t h = 0;

@@ -43,6 +43,13 @@ def test_version_string():
     assert "gfx950" in chunkfs_amd.version()
 
 
+def test_abi_version_matches_header():
+    from chunkfs_amd import _lib
+    m = re.search(r"#define CHUNKFS_AMD_ABI_VERSION (\d+)", open(HEADER).read())
+    assert m and _lib.lib().cdc_abi_version() == int(m.group(1))
+    assert f"abi {m.group(1)}" in _lib.lib().cdc_version().decode()
+
+
 def test_header_compiles_as_c():
     src = '#include "chunkfs_amd.h"\nint main(void){cdc_chunk_t c={0,0};(void)c;return sizeof(cdc_chunk_t)==16?0:1;}\n'
     exe = "/tmp/_abi_c_test"

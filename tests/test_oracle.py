@@ -142,3 +142,15 @@ def test_threaded_cpu_baseline_helper():
     data = oracle.splitmix64_bytes(8 << 20, 3)
     nb, wall = oracle.time_fastcdc_threads(data, 4096, 8192, 16384, threads=4, seconds=0.2)
     assert nb >= data.size and nb % (data.size // 4) == 0 and wall > 0
+
+
+def test_synthetic_generator_matches_oracle_and_device_fill_definition():
+    """chunkfs_amd.synthetic (bench / config-3 data) = the oracle's splitmix64
+    bytes = the definition of cdc_fill_splitmix64_device."""
+    from chunkfs_amd import synthetic
+    for n, seed in [(0, 1), (1, 1), (7, 3), (8, 3), (12345, 99), (1 << 16, 1000)]:
+        assert np.array_equal(synthetic.splitmix64_bytes(n, seed), oracle.splitmix64_bytes(n, seed))
+    vs = synthetic.versioned_archive(1 << 20, 3, seed=5)
+    assert len(vs) == 3 and vs[0].size == 1 << 20
+    assert all(abs(v.size - (1 << 20)) < (1 << 20) // 20 for v in vs)
+    assert not np.array_equal(vs[1][:100000], vs[2][:100000]) or not np.array_equal(vs[0], vs[1])
