@@ -7,7 +7,8 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libchunkfs_amd.so")
+# CHUNKFS_AMD_LIB: an experiment build of the same sources (tools/scan_variants.sh)
+LIB_PATH = os.environ.get("CHUNKFS_AMD_LIB") or os.path.join(HERE, "libchunkfs_amd.so")
 
 CDC_OK = 0
 CDC_EINVAL = -1

@@ -44,8 +44,12 @@ def _run(cmd):
     subprocess.check_call(cmd)
 
 
-def build(force=False):
-    os.makedirs(BUILD, exist_ok=True)
+def build(force=False, defines=(), lib=None, build_dir=None):
+    """Compile every source for gfx950 and link LIB (or `lib`: experiment
+    builds with extra -D `defines` into their own `build_dir`)."""
+    bdir = build_dir or BUILD
+    out_lib = lib or LIB
+    os.makedirs(bdir, exist_ok=True)
     common = [os.path.join(CSRC, h) for h in HEADERS] + [
         os.path.join(ROOT, "include", "chunkfs_amd.h"),
         os.path.join(ROOT, "include", "chunkfs_amd_tables.h"),
@@ -55,14 +59,14 @@ def build(force=False):
     objs = []
     for src in SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(BUILD, src + ".o")
+        o = os.path.join(bdir, src + ".o")
         objs.append(o)
         if force or _newer(o, [s] + common):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            _run([HIPCC] + CFLAGS + lang + ["-c", s, "-o", o])
-    if force or _newer(LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
-    return LIB
+            _run([HIPCC] + CFLAGS + [f"-D{d}" for d in defines] + lang + ["-c", s, "-o", o])
+    if force or _newer(out_lib, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_lib] + objs)
+    return out_lib
 
 
 if __name__ == "__main__":

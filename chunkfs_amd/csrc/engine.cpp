@@ -25,7 +25,10 @@ namespace cdc {
 namespace {
 thread_local std::string g_last_error;
 
-constexpr uint32_t kMinSpanLog2 = 16;  // 64 KiB spans at least
+#ifndef CDC_MIN_SPAN_LOG2
+#define CDC_MIN_SPAN_LOG2 16
+#endif
+constexpr uint32_t kMinSpanLog2 = CDC_MIN_SPAN_LOG2;  // 64 KiB spans at least (experiment builds may raise it)
 
 // fastcdc 3.1.0 v2020 FastCDC::new asserts (VERIFY).
 constexpr uint32_t kMinimumMin = 64, kMinimumMax = 1048576;

@@ -54,7 +54,19 @@ __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Experiment builds (tools/scan_variants.sh) may override the scheduling
+// fences, the lookahead and the waves per CU; defaults are the measured best.
+#ifndef CDC_SCAN_NOFENCE
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SCHED_FENCE() do {} while (0)
+#endif
+#ifndef CDC_SCAN_WAVES
+#define CDC_SCAN_WAVES 16
+#endif
+#ifndef CDC_SCAN_LOOK
+#define CDC_SCAN_LOOK 1
+#endif
 
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -186,6 +198,12 @@ struct EntryList {
     uint32_t *pos, *hlo, *hhi, *cnt;
 };
 
+// Entry word: quarter position in the span | kEntFix for the carry-in
+// fix-up's quarters (exact hash).  Main-loop entries in a lane's first 48
+// positions were hashed without the carry-in and are dropped by the flush.
+constexpr uint32_t kEntFix = 1u << 31;
+constexpr uint32_t kEntPos = kEntFix - 1;
+
 // Append (quarter position, hash before the quarter) for every lane whose
 // quarter hit; ne is wave-uniform.
 __device__ __forceinline__ void append_hits(bool hit, uint32_t pos, uint64_t h0, uint32_t &ne,
@@ -235,13 +253,15 @@ __device__ __forceinline__ uint32_t quarter(uint64_t &h, const uint4 &v, const u
 // One 64-byte step of a lane (4 quarters in C), lookups one dword ahead of
 // the chain across the whole step (8 VGPRs per group keeps the kernel
 // within 128 VGPRs = 16 waves per CU; the other waves cover LDS latency).
-// Quarters 0..skip-1 are left to the fix-up.
+// Step 0's quarters 0..2 (the lane's first 48 positions, hashed without the
+// carry-in) may append spurious entries: the flush drops them, and the
+// carry-in fix-up appends the exact ones (kEntFix).
 struct Q4 {
     uint4 q[4];
 };
 
 template <bool kAlign, int kLook>
-__device__ __forceinline__ void process_step(const Q4 &C, uint64_t &h, uint32_t pos0, uint32_t skip, uint32_t &ne,
+__device__ __forceinline__ void process_step(const Q4 &C, uint64_t &h, uint32_t pos0, uint32_t &ne,
                                              const EntryList &E, const uint64_t *tab, uint32_t rep,
                                              const FastParams &fp) {
     if constexpr (kLook == 1) {
@@ -265,7 +285,7 @@ __device__ __forceinline__ void process_step(const Q4 &C, uint64_t &h, uint32_t 
                 chain4_test<kAlign>(h, acc, gb, fp);
                 SCHED_FENCE();
             }
-            append_hits(acc == 0 && (uint32_t)q >= skip, pos0 + 16 * q, h0, ne, E);
+            append_hits(acc == 0, pos0 + 16 * q, h0, ne, E);
         }
     } else {
         // two dwords (8 lookups) ahead of the chain
@@ -291,13 +311,14 @@ __device__ __forceinline__ void process_step(const Q4 &C, uint64_t &h, uint32_t 
             chain4_test<kAlign>(h, acc, gb0, fp);
             chain4_test<kAlign>(h, acc, gb1, fp);
             SCHED_FENCE();
-            append_hits(acc == 0 && (uint32_t)q >= skip, pos0 + 16 * q, h0, ne, E);
+            append_hits(acc == 0, pos0 + 16 * q, h0, ne, E);
         }
     }
 }
 
 // The 4 coalesced loads of step t: instruction i reads piece (lane%4) of the
-// step of segment 16 i + lane/4 (16 complete 64-byte pieces per instruction).
+// step of segment 16 i + rsel(lane/4) (16 complete 64-byte pieces per
+// instruction; rsel: see the kernel).
 __device__ __forceinline__ void gload_step(Q4 &X, const uint8_t *gp, uint64_t istride, uint32_t t) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) X.q[i] = ld16(as_global4(gp + i * istride + t * kStep));
@@ -305,9 +326,10 @@ __device__ __forceinline__ void gload_step(Q4 &X, const uint8_t *gp, uint64_t is
 
 // Transpose through the wave's LDS tile: row o (80 bytes: 64 data + 16 pad)
 // holds segment o's step.  Rows are 20 dwords apart, so both directions are
-// bank-conflict free (ds_write_b128: 8 contiguous lanes = 2 rows x 64 B on
-// 32 distinct banks; ds_read_b128: 16 lanes of distinct l mod 16 start 20 l
-// mod 64 apart = 16 distinct 4-bank groups), and every address is a per-lane
+// bank-conflict free (ds_write_b128, banks (a/4) mod 32: an 8-lane group
+// writes rows x and x+4, 80 dwords = 16 banks apart, 32 distinct banks;
+// ds_read_b128: 16 lanes of distinct l mod 16 start 20 l mod 64 apart = 16
+// distinct 4-bank groups), and every address is a per-lane
 // base plus an immediate.  LDS is in order per wave, so the reads see the
 // writes and the next step's writes land after these reads; the barriers
 // only keep the compiler from moving LDS traffic across them.
@@ -322,8 +344,8 @@ __device__ __forceinline__ void stage_step(Q4 &C, const Q4 &X, uint4 *wrow, cons
 
 // Flush of one span: exact mask_s / mask_l flags for each hitting quarter
 // (re-hashed from the hash before it), position order, HBM write.
-__device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint32_t span_len, uint32_t ne,
-                                           const EntryList &E, const uint64_t *tab, uint32_t rep,
+__device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint32_t span_len, uint32_t sub_mask,
+                                           uint32_t ne, const EntryList &E, const uint64_t *tab, uint32_t rep,
                                            const FastParams &fp, const Candidates &cand, uint32_t lane) {
     wave_sync_lds();
     uint32_t *cpos = cand.pos + g * cand.cap;
@@ -333,8 +355,13 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
         return;
     }
     uint32_t hs = 0, hl = 0, my_pos = 0;
-    if (lane < ne) {
-        my_pos = E.pos[lane];
+    const uint32_t wd = lane < ne ? E.pos[lane] : 0u;
+    // (sub_mask = lane sub-span - 1; entries of the main loop at a lane's
+    // first 48 positions lack the carry-in: dropped, count 0)
+    const bool keep = lane < ne && ((wd & kEntFix) || (wd & sub_mask) >= 48);
+    if (lane < ne) E.cnt[lane] = 0;
+    if (keep) {
+        my_pos = wd & kEntPos;
         uint64_t hh = ((uint64_t)E.hhi[lane] << 32) | E.hlo[lane];
         const uint4 v = ld16_guarded(base, my_pos, span_len);
 #pragma unroll
@@ -357,9 +384,9 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
     for (uint32_t k = 0; k < ne; ++k) {
         const uint32_t c = E.cnt[k];
         total += c;
-        if (E.pos[k] < my_pos) slot += c;
+        if ((E.pos[k] & kEntPos) < my_pos) slot += c;
     }
-    if (lane < ne) {
+    if (keep) {
         for (uint32_t m = hs | hl; m; m &= m - 1) {
             const uint32_t j = __builtin_ctz(m);
             if (slot < cand.cap)
@@ -406,7 +433,13 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
     const uint32_t lo = lane << sub_log2;  // lane's first byte in the span
     const uint64_t istride = 16ull * sub;
     const EntryList E{L.epos[wave], L.ehlo[wave], L.ehhi[wave], L.ecnt[wave]};
-    uint4 *wrow = &L.stage[wave][(lane >> 2) * 5 + (lane & 3)];
+    // Instruction i's lane quad u = lane/4 loads row 16 i + rsel(u); the two
+    // quads of one ds_write_b128 lane group (8 lanes) get rows 4 apart, so
+    // their 80-byte rows sit 16 banks apart and the write is conflict-free
+    // (rows u, u+1 collided on one 4-bank group: 8 extra LDS cycles per
+    // store, r02av PMC); the reads (lane = row) are unchanged.
+    const uint32_t rsel = ((lane >> 3) & 3) + 8 * (lane >> 5) + 4 * ((lane >> 2) & 1);
+    uint4 *wrow = &L.stage[wave][rsel * 5 + (lane & 3)];
     const uint4 *rrow = &L.stage[wave][lane * 5];
 
     // Spans are software-pipelined: the first two steps of the next span are
@@ -427,7 +460,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
     const uint8_t *base = nullptr, *gp = nullptr;
     auto prefetch = [&]() {  // first two steps and the carry bytes of span g
         base = st.ptrs[si] + off;
-        gp = base + (uint64_t)(lane >> 2) * sub + (lane & 3) * 16;
+        gp = base + (uint64_t)rsel * sub + (lane & 3) * 16;
         wb = 0;
         if (off != 0 && lane < 48) wb = as_global1(base)[(int)lane - 48];
         gload_step(A, gp, istride, 0);
@@ -452,19 +485,19 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         SCHED_FENCE();
 // kMode: 0 = the scan; 1 = loads and transposes only, 2 = hashing only (timing
 // experiments: CHUNKFS_AMD_DIAG bits 8-9, results meaningless).
-#define CDC_PROC(POS, SKIP)                                                                    \
+#define CDC_PROC(POS)                                                                          \
     do {                                                                                       \
         if constexpr (kMode == 1) h ^= (uint64_t)(C.q[0].x ^ C.q[1].y ^ C.q[2].z ^ C.q[3].w);   \
-        else process_step<kAlign, kLook>(C, h, POS, SKIP, ne, E, tab, rep, fp);                \
+        else process_step<kAlign, kLook>(C, h, POS, ne, E, tab, rep, fp);                      \
     } while (0)
 #define CDC_SCAN_PAIR(T, LOAD_B, STAGE_A, LOAD_A)                                              \
     do {                                                                                       \
-        CDC_PROC(lo + (T) * kStep, (T) == 0 ? 3u : 0u);                                        \
+        CDC_PROC(lo + (T) * kStep);                                                            \
         SCHED_FENCE();                                                                         \
         stage_step(C, B, wrow, rrow);                                                          \
         if (LOAD_B && kMode != 2) gload_step(B, gp, istride, (T) + 3);                         \
         SCHED_FENCE();                                                                         \
-        CDC_PROC(lo + ((T) + 1) * kStep, 0u);                                                  \
+        CDC_PROC(lo + ((T) + 1) * kStep);                                                      \
         SCHED_FENCE();                                                                         \
         if (STAGE_A) stage_step(C, A, wrow, rrow);                                             \
         if (LOAD_A && kMode != 2) gload_step(A, gp, istride, (T) + 4);                         \
@@ -488,13 +521,13 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         h = wave_shr1(h, off_cur != 0 ? hw : 0);
         {
             uint64_t h0 = h;
-            append_hits(quarter<kAlign>(h, F0, tab, rep, fp) == 0, lo, h0, ne, E);
+            append_hits(quarter<kAlign>(h, F0, tab, rep, fp) == 0, lo | kEntFix, h0, ne, E);
             h0 = h;
-            append_hits(quarter<kAlign>(h, F1, tab, rep, fp) == 0, lo + 16, h0, ne, E);
+            append_hits(quarter<kAlign>(h, F1, tab, rep, fp) == 0, (lo + 16) | kEntFix, h0, ne, E);
             h0 = h;
-            append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, lo + 32, h0, ne, E);
+            append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, (lo + 32) | kEntFix, h0, ne, E);
         }
-        flush_span(g_cur, base_cur, (uint32_t)span, ne, E, tab, rep, fp, cand, lane);
+        flush_span(g_cur, base_cur, (uint32_t)span, sub - 1, ne, E, tab, rep, fp, cand, lane);
     }
 }
 
@@ -534,9 +567,9 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
         bool hit = false;
         const uint64_t h0 = h;
         if (active && p < span_len) hit = quarter<kAlign>(h, ld16_guarded(base, p, span_len), tab, rep, fp) == 0;
-        append_hits(hit, p, h0, ne, E);
+        append_hits(hit, p | kEntFix, h0, ne, E);
     }
-    flush_span(g, base, span_len, ne, E, tab, rep, fp, cand, lane);
+    flush_span(g, base, span_len, 0, ne, E, tab, rep, fp, cand, lane);
 }
 
 
@@ -1491,7 +1524,7 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
     }
     // 16 waves per CU (the 128-VGPR budget), GEAR lookups one dword ahead of
     // the chain.  (Measured: 12 waves with two dwords of lookahead is slower.)
-    constexpr int W = 16, K = 1;
+    constexpr int W = CDC_SCAN_WAVES, K = CDC_SCAN_LOOK;
     const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
     const uint32_t mode = (fp.diag >> 8) & 3;

@@ -20,7 +20,7 @@ rc=$?; echo "bench rc=$rc"; cat $OUT/bench_$TAG.json; tail -3 $OUT/bench_$TAG.er
 [ $rc -eq 0 ] || exit $rc
 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --no-host-path --no-sweep --no-algos \
+    python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-parity --no-host-path --no-sweep --no-algos --no-config4 \
     > $OUT/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 $OUT/prof_$TAG.log
 exit $rc

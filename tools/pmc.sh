@@ -10,7 +10,7 @@ run() {  # name, counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" --output-format csv \
       -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity --no-host-path --no-algos \
-      --no-sweep > $OUT/$name.log 2>&1
+      --no-sweep --no-config4 > $OUT/$name.log 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   return $rc
