@@ -132,6 +132,7 @@ class DeviceEngine:
         self.dev = torch.device("cuda", local)
         self.local = local
         self.ch = cfa.FastChunker(cfa.SizeParams(args.min, args.avg, args.max), device=local)
+        self.sizes = (args.min, args.avg, args.max)
 
     def prepare(self, lens, seeds):
         import numpy as np
@@ -535,11 +536,19 @@ def config3_line(args, local, base_bytes=256 << 20, versions=16):
 
 def host_path_leg(eng, w):
     """PCIe-inclusive rates of the host boundary, recorded beside `value`,
-    never as it: cdc_chunk_data on a 1 GiB host buffer, and the
-    reference harness's own measure -- the StorageWriter loop over 1 MiB
-    segments, bytes / summed chunk_data seconds (src/bench/mod.rs:93-140,
-    src/system/storage.rs:314-316)."""
+    never as it (DESIGN.md):
+      * cdc_chunk_data on the whole 1 GiB host buffer;
+      * chunk_data_1MiB_calls: the Rust shim's own loop -- StorageWriter::write
+        per 1 MiB segment (buffer = rest ++ segment, chunk_data, rest = last
+        chunk; storage.rs:302-357) timed like the reference, Sum of the
+        chunk_data calls only (storage.rs:314-316, report.rs:168-175);
+      * write_stream_1MiB_segments: the same write through the streaming path
+        (cdc_write_segment per 1 MiB segment, wall time begin -> finish).
+    Spans are checked against the oracle's StorageWriter loop."""
+    import numpy as np
     import chunkfs_amd as cfa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
     hb = w.bufs[0][:w.lens[0]].cpu().numpy()
     ch = eng.ch
     ch.chunk_array(hb)
@@ -548,14 +557,47 @@ def host_path_leg(eng, w):
         hc = ch.chunk_array(hb)
     t_h = (time.perf_counter() - t_h) / reps
     hp = {"GiBps": hb.size / t_h / (1 << 30), "bytes": int(hb.size), "chunks": int(hc.shape[0]),
-          "entry": "cdc_chunk_data (pageable host buffer -> H2D -> pipeline -> D2H chunks)"}
+          "entry": "cdc_chunk_data (pageable host buffer -> pinned ring -> H2D -> pipeline -> host-mapped chunk list)"}
     fs_bytes = min(hb.size, 256 << 20)
-    spans, chunk_s = cfa.write_spans(ch, hb[:fs_bytes])
-    hp["fs_write_1MiB_segments"] = {
-        "GiBps": fs_bytes / chunk_s / (1 << 30), "bytes": int(fs_bytes), "spans": int(spans.size),
-        "metric": "bytes / wall seconds of cdc_fs_write (pageable host buffer -> H2D -> chunking -> D2H of "
-                  "the chunk list); spans identical to the reference's 1 MiB StorageWriter loop "
-                  "(tests/test_gpu_parity.py::test_write_path_segmentation_invariance)"}
+    seg = 1 << 20
+    ref_spans, ref_secs = oracle.fs_write("fast", hb[:fs_bytes], *eng.sizes)
+    # the reference loop through cdc_chunk_data
+    for rnd in range(2):  # (round 0 warms the buffers)
+        spans, rest, chunk_s = [], np.empty(0, dtype=np.uint8), 0.0
+        st0 = cfa.host_stats(ch)
+        for off in range(0, fs_bytes, seg):
+            buf = np.concatenate([rest, hb[off:off + seg]])
+            t0 = time.perf_counter()
+            chunks = ch.chunk_array(buf)
+            chunk_s += time.perf_counter() - t0
+            spans += [int(x) for x in chunks[:-1, 1]]
+            o, ln = (int(x) for x in chunks[-1])
+            rest = buf[o:o + ln]
+        spans.append(int(rest.size))
+        st1 = cfa.host_stats(ch)
+    calls = st1["calls"] - st0["calls"]
+    hp["chunk_data_1MiB_calls"] = {
+        "GiBps": fs_bytes / chunk_s / (1 << 30), "bytes": int(fs_bytes), "calls": calls,
+        "us_per_call": chunk_s / calls * 1e6,
+        "upload_us_per_call": (st1["upload_s"] - st0["upload_s"]) / calls * 1e6,
+        "spans_equal_oracle_fs_write": spans == [int(x) for x in ref_spans],
+        "cpu_oracle_same_loop_GiBps": fs_bytes / ref_secs / (1 << 30),
+        "metric": "bytes / summed seconds inside cdc_chunk_data over the reference's 1 MiB StorageWriter loop "
+                  "(what CDCFixture::measure reports as chunk throughput); each call = CPU copy into pinned memory, "
+                  "H2D, scan + resolve, chunk list in host-mapped memory"}
+    # the streaming write path over the whole 1 GiB
+    for rnd in range(2):
+        sw = cfa.StreamWriter(ch)
+        for off in range(0, hb.size, seg):
+            sw.write(hb[off:off + seg])
+        sspans, ssecs = sw.finish()
+    whole = hc[:, 1]
+    hp["write_stream_1MiB_segments"] = {
+        "GiBps": hb.size / ssecs / (1 << 30), "bytes": int(hb.size), "spans": int(sspans.size),
+        "spans_equal_whole_stream": bool(sspans.shape == whole.shape and (sspans == whole).all()),
+        "metric": "bytes / wall seconds cdc_write_begin -> cdc_write_finish, 1 MiB cdc_write_segment calls "
+                  "(CPU copy into the pinned ring, async H2D, device chunking of 256 MiB windows, carried chunk "
+                  "in HBM)"}
     return hp
 
 
@@ -644,9 +686,10 @@ def main(argv=None):
             extras["config5_1gpu"] = config5_lines(args, eng, w)
         if args.cpu_seconds > 0:
             extras["cpu_baseline"] = cpu_baseline_leg(args, w.bufs[0][:shard.lens[0]].cpu().numpy())
-            fw = extras.get("host_path", {}).get("fs_write_1MiB_segments")
-            if fw:
-                fw["x_cpu_single_thread"] = fw["GiBps"] / extras["cpu_baseline"]["value"]
+            for k in ("chunk_data_1MiB_calls", "write_stream_1MiB_segments"):
+                fw = extras.get("host_path", {}).get(k)
+                if fw:
+                    fw["x_cpu_single_thread"] = fw["GiBps"] / extras["cpu_baseline"]["value"]
 
     if args.rank_parity and not args.stub:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

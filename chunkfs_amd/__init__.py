@@ -33,7 +33,7 @@ SEG_SIZE = MB  # src/lib.rs:39
 __all__ = [
     "KB", "MB", "GB", "SEG_SIZE", "Chunk", "SizeParams", "Chunker", "FastChunker",
     "FSChunker", "RabinChunker", "SuperChunker", "UltraChunker", "LeapChunker",
-    "SeqChunker", "OperationMode", "SeqConfig", "CdcError", "write_spans", "version",
+    "SeqChunker", "OperationMode", "SeqConfig", "CdcError", "write_spans", "StreamWriter", "version",
 ]
 
 
@@ -317,9 +317,11 @@ class SuperChunker(Chunker):
 
 
 def write_spans(chunker, data, seg_size=SEG_SIZE):
-    """ChunkStorage::write (storage.rs:78-103) for one write call.
+    """ChunkStorage::write (storage.rs:78-103) for one write call (seg_size
+    segments through the streaming write path).
 
-    Returns (span lengths in file order, seconds spent inside chunk_data).
+    Returns (span lengths in file order, wall seconds of the whole call: host
+    copy + H2D + chunking, not the reference's chunk_data-only time).
     """
     ptr, n, keep = _as_buffer(data)
     cap = chunker.max_chunk_count(n) + 1  # spans are chunks: all but the last are >= min
@@ -331,6 +333,43 @@ def write_spans(chunker, data, seg_size=SEG_SIZE):
     del keep
     assert cnt <= cap
     return out[:cnt], secs.value
+
+
+class StreamWriter:
+    """One file write through the streaming write path (cdc_write_begin /
+    cdc_write_segment / cdc_write_finish): ChunkStorage::write_from_stream
+    (storage.rs:105-137) with StorageWriter::write per segment and
+    StorageWriter::flush at the end (storage.rs:302-383).  Segments are copied
+    into a pinned ring and uploaded while the caller continues; finish()
+    returns (span lengths in file order, wall seconds since begin)."""
+
+    def __init__(self, chunker):
+        self._ch = chunker
+        self._bytes = 0
+        check(lib().cdc_write_begin(chunker._h))
+
+    def write(self, segment):
+        ptr, n, keep = _as_buffer(segment)
+        check(lib().cdc_write_segment(self._ch._h, ptr, n))
+        del keep
+        self._bytes += n
+
+    def finish(self):
+        cap = self._ch.max_chunk_count(self._bytes) + 1
+        out = np.empty(max(cap, 1), dtype=np.uint64)
+        secs = ctypes.c_double(0.0)
+        cnt = check(lib().cdc_write_finish(self._ch._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap,
+                                           ctypes.byref(secs)))
+        assert cnt <= cap
+        return out[:cnt], secs.value
+
+
+def host_stats(chunker):
+    """cdc_debug_host_stats: chunk_data calls, upload s, total s; streaming
+    write chunking s and segments."""
+    v = (ctypes.c_double * 5)()
+    check(lib().cdc_debug_host_stats(chunker._h, v, 5))
+    return {"calls": int(v[0]), "upload_s": v[1], "total_s": v[2], "write_chunk_s": v[3], "write_segments": int(v[4])}
 
 
 class DedupIndex:

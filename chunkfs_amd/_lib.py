@@ -23,13 +23,14 @@ EXPORTS = [
     "cdc_create", "cdc_create_seq", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
     "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear",
     "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
-    "cdc_fs_write", "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
+    "cdc_fs_write", "cdc_write_begin", "cdc_write_segment", "cdc_write_finish",
+    "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
     "cdc_index_create", "cdc_index_destroy", "cdc_index_clear", "cdc_index_insert_device",
     "cdc_index_stats",
     "cdc_fill_splitmix64_device", "cdc_version", "cdc_abi_version",
 ]
 # include/chunkfs_amd_debug.h (diagnostics, not part of the drop-in boundary)
-DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy"]
+DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy", "cdc_debug_host_stats"]
 
 
 class CdcError(RuntimeError):
@@ -118,6 +119,14 @@ def lib():
     L.cdc_last_timing.restype = ctypes.c_int
     L.cdc_fs_write.argtypes = [P, P, sz, sz, u64p, sz, ctypes.POINTER(ctypes.c_double)]
     L.cdc_fs_write.restype = ctypes.c_int64
+    L.cdc_write_begin.argtypes = [P]
+    L.cdc_write_begin.restype = ctypes.c_int
+    L.cdc_write_segment.argtypes = [P, P, sz]
+    L.cdc_write_segment.restype = ctypes.c_int
+    L.cdc_write_finish.argtypes = [P, u64p, sz, ctypes.POINTER(ctypes.c_double)]
+    L.cdc_write_finish.restype = ctypes.c_int64
+    L.cdc_debug_host_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), sz]
+    L.cdc_debug_host_stats.restype = ctypes.c_int
     L.cdc_sha256_chunks_device.argtypes = [P, P, P, sz, P, P]
     L.cdc_sha256_chunks_device.restype = ctypes.c_int
     L.cdc_chunk_and_hash.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), u8p, sz]

@@ -106,6 +106,34 @@ int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
     return n;
 }
 
+int cdc_write_begin(cdc_handle_t *h) {
+    if (!h) return (int)bad_handle();
+    return h->engine->write_begin();
+}
+
+int cdc_write_segment(cdc_handle_t *h, const uint8_t *data, size_t len) {
+    if (!h) return (int)bad_handle();
+    return h->engine->write_segment(data, len);
+}
+
+int64_t cdc_write_finish(cdc_handle_t *h, uint64_t *span_lengths, size_t cap, double *seconds) {
+    if (!h) return bad_handle();
+    if (cap && !span_lengths) {
+        cdc::set_error("cdc_write_finish: span_lengths is NULL");
+        return CDC_EINVAL;
+    }
+    std::vector<uint64_t> spans;
+    const int64_t n = h->engine->write_finish(spans, seconds);
+    if (n < 0) return n;
+    for (size_t i = 0; i < spans.size() && i < cap; ++i) span_lengths[i] = spans[i];
+    return n;
+}
+
+int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n) {
+    if (!h || (n && !v)) return (int)bad_handle();
+    return h->engine->host_stats(v, n);
+}
+
 int cdc_sha256_chunks_device(cdc_handle_t *h, const uint8_t *d_data,
                              const cdc_chunk_t *d_chunks, size_t n_chunks,
                              uint8_t *d_digests, void *hip_stream) {

@@ -113,6 +113,12 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         if (const char *d = std::getenv("CHUNKFS_AMD_DIAG")) fp.diag = (uint32_t)std::atoi(d);
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
+        e->small_span_log2_ = l2 > 14 ? l2 : 14;
+        if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_SPAN")) {  // experiments: 0 = off
+            const int x = std::atoi(v);
+            e->small_span_log2_ = x == 0 ? e->span_log2_ : (uint32_t)std::max<int>(x, (int)std::max(l2, 14u));
+        }
+        if (e->small_span_log2_ > e->span_log2_) e->small_span_log2_ = e->span_log2_;
         const uint64_t span = 1ull << e->span_log2_;
         const uint32_t pc = (uint32_t)__builtin_popcountll(fp.cmask);
         uint64_t cap = 8 * (span >> (pc < 63 ? pc : 63));
@@ -181,6 +187,15 @@ Engine::~Engine() {
     (void)hipFree(d_wtabs_);
     (void)hipFree(wws_);
     (void)hipHostFree(h_stage_);
+    if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
+    (void)hipHostFree(h_ring_);
+    (void)hipHostFree(h_out_);
+    for (auto &w : ws_win_) (void)hipFree(w);
+    for (auto &e : ring_ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (copy_done_) (void)hipEventDestroy(copy_done_);
+    if (ws_ev_) (void)hipEventDestroy(ws_ev_);
+    if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     for (auto &ev : ev_)
         if (ev) (void)hipEventDestroy(ev);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
@@ -316,7 +331,12 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
     uint64_t *h_tails = h + 3 * h_stage_streams_;
-    const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? span_log2_ : is_walk() ? seg_log2_ : 0;
+    // Small FastCDC batches (the host path's 1 MiB chunk_data calls) use the
+    // shortest spans the kernels allow (>= max, >= 16 KiB: 256 B per scan
+    // lane): 4x the lanes and a 4x shorter serial scan per lane, for latency.
+    const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? (bytes <= kSmallBatch ? small_span_log2_ : span_log2_)
+                         : is_walk()               ? seg_log2_
+                                                   : 0;
     uint64_t spans = 0;
     uint32_t n_tails = 0;
     for (size_t i = 0; i < n; ++i) {
@@ -453,62 +473,6 @@ int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
     return CDC_OK;
 }
 
-int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out,
-                           size_t cap, uint8_t *digests) {
-    if (len && !data) {
-        set_error("cdc_chunk_data: data is NULL");
-        return CDC_EINVAL;
-    }
-    if (cap && !out) {
-        set_error("cdc_chunk_data: out is NULL");
-        return CDC_EINVAL;
-    }
-    if (len == 0) return 0;  // FastCDC iterator yields nothing; FSChunker loop never runs
-    HIP_TRY(hipSetDevice(device_));
-    if (d_data_bytes_ < len) {
-        (void)hipFree(d_data_);
-        d_data_ = nullptr;
-        d_data_bytes_ = 0;
-        const size_t want = align_up(len + len / 8, 1 << 20);
-        HIP_TRY(hipMalloc(&d_data_, want));
-        d_data_bytes_ = want;
-    }
-    const size_t need = max_chunks(len);
-    if (d_out_cap_ < need) {
-        (void)hipFree(d_out_);
-        d_out_ = nullptr;
-        d_out_cap_ = 0;
-        const size_t want = need + need / 8 + 64;
-        HIP_TRY(hipMalloc(&d_out_, want * sizeof(cdc_chunk_t)));
-        d_out_cap_ = want;
-    }
-    HIP_TRY(hipMemcpyAsync(d_data_, data, len, hipMemcpyHostToDevice, own_stream_));
-    const uint8_t *p = d_data_;
-    const uint64_t l = len;
-    uint64_t first[2] = {0, 0};
-    const int64_t count = chunk_batch_device(1, &p, &l, d_out_, d_out_cap_, first, own_stream_);
-    if (count < 0) return count;
-    const size_t copy = (size_t)count < cap ? (size_t)count : cap;
-    if (digests && copy) {
-        if (d_dig_cap_ < (size_t)count) {
-            (void)hipFree(d_dig_);
-            d_dig_ = nullptr;
-            d_dig_cap_ = 0;
-            const size_t want = (size_t)count + (size_t)count / 8 + 64;
-            HIP_TRY(hipMalloc(&d_dig_, want * 32));
-            d_dig_cap_ = want;
-        }
-        const int rc = sha256_device(d_data_, d_out_, (size_t)count, d_dig_, own_stream_);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(digests, d_dig_, copy * 32, hipMemcpyDeviceToHost, own_stream_));
-    }
-    if (copy) {
-        HIP_TRY(hipMemcpyAsync(out, d_out_, copy * sizeof(cdc_chunk_t), hipMemcpyDeviceToHost, own_stream_));
-        HIP_TRY(hipStreamSynchronize(own_stream_));
-    }
-    return count;
-}
-
 int64_t Engine::fs_write(const uint8_t *data, size_t len, size_t seg_size, std::vector<uint64_t> &spans,
                          double *seconds) {
     spans.clear();
@@ -520,24 +484,16 @@ int64_t Engine::fs_write(const uint8_t *data, size_t len, size_t seg_size, std::
         set_error("cdc_fs_write: data is NULL");
         return CDC_EINVAL;
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    constexpr size_t kFsWindow = size_t(1) << 32;  // bytes of the write per device pass
-    std::vector<cdc_chunk_t> chunks;
-    size_t rest = 0;  // start of the carried-over chunk: a chunk boundary of the whole write
-    for (size_t cur = 0; cur < len;) {
-        const size_t end = len - cur < kFsWindow ? len : cur + kFsWindow;
-        const size_t n = end - rest;  // buffer = rest ++ new bytes (storage.rs:309-310), contiguous here
-        chunks.resize(max_chunks(n));
-        const int64_t c = chunk_host(data + rest, n, chunks.data(), chunks.size());
-        if (c < 0) return c;
-        // storage.rs:318-322: every chunk but the last becomes a span, the last is carried
-        for (int64_t i = 0; i + 1 < c; ++i) spans.push_back(chunks[i].length);
-        if (c > 0) rest += chunks[c - 1].offset;
-        cur = end;
+    // ChunkStorage::write (storage.rs:84-100): StorageWriter::write per
+    // seg_size slice, then flush -- through the streaming write path.
+    int rc = write_begin();
+    for (size_t off = 0; !rc && off < len; off += seg_size)
+        rc = write_segment(data + off, std::min(seg_size, len - off));
+    if (rc) {
+        wr_.active = false;
+        return rc;
     }
-    if (len > rest) spans.push_back(len - rest);  // flush (storage.rs:360-383)
-    if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    return (int64_t)spans.size();
+    return write_finish(spans, seconds);
 }
 
 int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,

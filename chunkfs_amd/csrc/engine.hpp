@@ -33,14 +33,18 @@ class Engine {
     int64_t chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, size_t cap,
                        uint8_t *digests = nullptr);
     // ChunkStorage::write of one whole write (storage.rs:78-103, 302-383):
-    // the span lengths the StorageWriter loop produces.  Both supported
-    // chunkers restart at every chunk boundary, so the carried-over `rest`
-    // always begins at a boundary of the whole write and the spans do not
-    // depend on the segment size: the write is chunked in
-    // device windows of up to kFsWindow bytes, each window's last chunk
-    // carried into the next exactly as the reference carries `rest`.
+    // the span lengths of the StorageWriter loop over seg_size segments, run
+    // through the streaming write path below (hostpath.cpp).
     int64_t fs_write(const uint8_t *data, size_t len, size_t seg_size, std::vector<uint64_t> &spans,
                      double *seconds);
+    // Streaming write path (hostpath.cpp): one file write as a sequence of
+    // segments (write_from_stream, storage.rs:105-137); spans at finish.
+    int write_begin();
+    int write_segment(const uint8_t *data, size_t len);
+    int64_t write_finish(std::vector<uint64_t> &spans, double *seconds);
+    // Host-path statistics: calls, upload s, total s of chunk_host; chunking s
+    // and segments of the current / last streaming write.
+    int host_stats(double *v, size_t n) const;
     // SHA-256 of chunks of one device-resident stream (Sha256Hasher::hash).
     int sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
                       uint8_t *d_digests, hipStream_t s);
@@ -82,6 +86,12 @@ class Engine {
     int init_walk(const uint32_t *seq);
     int ensure_walk_workspace(uint64_t segs, size_t n);
     int run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64_t *first, hipStream_t s);
+    // Host boundary (hostpath.cpp).
+    int ensure_ring();
+    int ensure_host_out(size_t chunks);
+    int ensure_device_data(size_t len);
+    int upload(const uint8_t *src, size_t len, uint8_t *dst, hipStream_t s, size_t piece);
+    int write_window(bool final);
 
     cdc_algo_t algo_ = CDC_ALGO_FASTCDC;
     uint32_t min_ = 0, avg_ = 0, max_ = 0;
@@ -89,6 +99,8 @@ class Engine {
     int num_cus_ = 256;
     FastParams fp_{};
     uint32_t span_log2_ = 16;
+    uint32_t small_span_log2_ = 16;                       // spans of batches <= kSmallBatch bytes
+    static constexpr uint64_t kSmallBatch = uint64_t(8) << 20;
     uint32_t cap_ = 0, smax_ = 0;
     std::string describe_;
 
@@ -119,7 +131,33 @@ class Engine {
     void *h_stage_ = nullptr;
     size_t h_stage_streams_ = 0;
 
-    // Host-path buffers (cdc_chunk_data).
+    // Host path (hostpath.cpp): pinned upload ring (slot k reused once its
+    // DMA event completes), host-mapped chunk output written by the kernels,
+    // a copy stream for the streaming writes and two device windows.
+    static constexpr uint32_t kRingSlots = 4;
+    static constexpr size_t kRingSlot = size_t(4) << 20;
+    static constexpr size_t kWriteWindow = size_t(256) << 20;
+    static constexpr size_t kRingDirect = size_t(16) << 20;  // chunk_data above this: pageable hipMemcpyAsync
+    void *h_ring_ = nullptr;
+    hipEvent_t ring_ev_[kRingSlots] = {};
+    uint32_t ring_next_ = 0;
+    hipStream_t copy_stream_ = nullptr;
+    hipEvent_t copy_done_ = nullptr, ws_ev_ = nullptr;
+    cdc_chunk_t *h_out_ = nullptr, *d_hout_ = nullptr;
+    size_t h_out_cap_ = 0;
+    uint8_t *ws_win_[2] = {nullptr, nullptr};
+    struct WriteState {
+        bool active = false;
+        int cur = 0;
+        size_t reserve = 0, carry = 0, fill = 0;
+        uint64_t bytes = 0, segments = 0;
+        double t0 = 0, chunk_s = 0;
+        std::vector<uint64_t> spans;
+    } wr_;
+    struct HostStats {
+        uint64_t calls = 0;
+        double upload_s = 0, total_s = 0;
+    } host_;
     uint8_t *d_data_ = nullptr;
     size_t d_data_bytes_ = 0;
     cdc_chunk_t *d_out_ = nullptr;

@@ -1,0 +1,276 @@
+// hostpath.cpp -- the host-memory boundary of the engine:
+// Chunker::chunk_data on a host buffer (reference src/lib.rs:80, called by
+// StorageWriter::write, src/system/storage.rs:302-357) and the write path of
+// one file (ChunkStorage::write / write_from_stream, storage.rs:78-137) as a
+// streaming, overlapped upload.
+//
+//   upload       pageable caller bytes -> handle-owned pinned ring (CPU memcpy,
+//                one slot per piece) -> async H2D on the engine stream; the
+//                copy of piece k+1 runs while piece k's DMA is in flight
+//   chunk_host   upload + the device pipeline; the chunk list is written by
+//                the kernels straight into host-mapped pinned memory (no D2H
+//                copy, no extra sync)
+//   write_*      StorageWriter over a stream of segments: bytes accumulate in
+//                a device window (double-buffered) while later segments
+//                upload; a full window is chunked on the device, every chunk
+//                but the last becomes a span and the last one is carried into
+//                the next window in HBM (the reference's `rest`, storage.rs:
+//                309-322); finish = flush (storage.rs:360-383).
+//
+// The spans equal the reference's per-segment loop for any segment sizes: every
+// chunker here restarts at each chunk boundary and looks only forward, so a
+// window's chunks other than its last are the whole write's (SURVEY.md A.4,
+// tests/test_gpu_hostpath.py).
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "engine.hpp"
+
+namespace cdc {
+
+#define HIP_TRY(expr)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) {                                                \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(e_));      \
+            return CDC_EDEVICE;                                                \
+        }                                                                      \
+    } while (0)
+
+namespace {
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+int Engine::ensure_ring() {
+    if (h_ring_) return CDC_OK;
+    HIP_TRY(hipHostMalloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocDefault));
+    for (auto &e : ring_ev_) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&copy_done_, hipEventDisableTiming));
+    return CDC_OK;
+}
+
+int Engine::ensure_host_out(size_t chunks) {
+    if (h_out_ && h_out_cap_ >= chunks) return CDC_OK;
+    (void)hipHostFree(h_out_);
+    h_out_ = nullptr;
+    d_hout_ = nullptr;
+    h_out_cap_ = 0;
+    const size_t want = round_up(chunks + chunks / 8 + 64, 4096);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_out_), want * sizeof(cdc_chunk_t), hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_hout_), h_out_, 0));
+    h_out_cap_ = want;
+    return CDC_OK;
+}
+
+int Engine::ensure_device_data(size_t len) {
+    if (d_data_bytes_ >= len) return CDC_OK;
+    (void)hipFree(d_data_);
+    d_data_ = nullptr;
+    d_data_bytes_ = 0;
+    const size_t want = round_up(len + len / 8, size_t(1) << 20);
+    HIP_TRY(hipMalloc(&d_data_, want));
+    d_data_bytes_ = want;
+    return CDC_OK;
+}
+
+// Pageable host bytes -> pinned ring slot -> async H2D (stream s).  Pieces of
+// `piece` bytes (<= kRingSlot); a slot is reused once its previous DMA is done.
+int Engine::upload(const uint8_t *src, size_t len, uint8_t *dst, hipStream_t s, size_t piece) {
+    for (size_t off = 0; off < len;) {
+        const size_t n = std::min(piece, len - off);
+        const uint32_t k = ring_next_;
+        ring_next_ = (ring_next_ + 1) % kRingSlots;
+        HIP_TRY(hipEventSynchronize(ring_ev_[k]));  // (an event never recorded is complete)
+        uint8_t *slot = static_cast<uint8_t *>(h_ring_) + (size_t)k * kRingSlot;
+        std::memcpy(slot, src + off, n);
+        HIP_TRY(hipMemcpyAsync(dst + off, slot, n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipEventRecord(ring_ev_[k], s));
+        off += n;
+    }
+    return CDC_OK;
+}
+
+int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, size_t cap, uint8_t *digests) {
+    if (len && !data) {
+        set_error("cdc_chunk_data: data is NULL");
+        return CDC_EINVAL;
+    }
+    if (cap && !out) {
+        set_error("cdc_chunk_data: out is NULL");
+        return CDC_EINVAL;
+    }
+    if (len == 0) return 0;  // FastCDC iterator yields nothing; FSChunker loop never runs
+    HIP_TRY(hipSetDevice(device_));
+    const double t0 = now_s();
+    int rc = ensure_ring();
+    if (!rc) rc = ensure_device_data(len);
+    const size_t need = max_chunks(len);
+    if (!rc) rc = ensure_host_out(need);
+    if (rc) return rc;
+    // Small calls (the reference's 1 MiB segments) go through the pinned ring
+    // in 256 KiB pieces, so that the CPU copy of one piece overlaps the DMA of
+    // the previous one; large buffers take HIP's own pageable path, which
+    // stages with several threads (measured 51 vs 31 GiB/s for the single-
+    // thread ring on 1 GiB).
+    if (len <= kRingDirect) {
+        rc = upload(data, len, d_data_, own_stream_, 256u << 10);
+        if (rc) return rc;
+    } else {
+        HIP_TRY(hipMemcpyAsync(d_data_, data, len, hipMemcpyHostToDevice, own_stream_));
+    }
+    const double t1 = now_s();
+    const uint8_t *p = d_data_;
+    const uint64_t l = len;
+    uint64_t first[2] = {0, 0};
+    const int64_t count = chunk_batch_device(1, &p, &l, reinterpret_cast<cdc_chunk_t *>(d_hout_), need, first,
+                                             own_stream_);
+    if (count < 0) return count;
+    const size_t copy = (size_t)count < cap ? (size_t)count : cap;
+    if (digests && copy) {
+        if (d_out_cap_ < (size_t)count) {  // the SHA-256 kernel reads the chunk list from HBM
+            (void)hipFree(d_out_);
+            d_out_ = nullptr;
+            d_out_cap_ = 0;
+            const size_t want = (size_t)count + (size_t)count / 8 + 64;
+            HIP_TRY(hipMalloc(&d_out_, want * sizeof(cdc_chunk_t)));
+            d_out_cap_ = want;
+        }
+        if (d_dig_cap_ < (size_t)count) {
+            (void)hipFree(d_dig_);
+            d_dig_ = nullptr;
+            d_dig_cap_ = 0;
+            const size_t want = (size_t)count + (size_t)count / 8 + 64;
+            HIP_TRY(hipMalloc(&d_dig_, want * 32));
+            d_dig_cap_ = want;
+        }
+        HIP_TRY(hipMemcpyAsync(d_out_, h_out_, (size_t)count * sizeof(cdc_chunk_t), hipMemcpyHostToDevice,
+                               own_stream_));
+        rc = sha256_device(d_data_, d_out_, (size_t)count, d_dig_, own_stream_);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy(digests, d_dig_, copy * 32, hipMemcpyDeviceToHost));
+    }
+    if (copy) std::memcpy(out, h_out_, copy * sizeof(cdc_chunk_t));
+    host_.calls += 1;
+    host_.upload_s += t1 - t0;
+    host_.total_s += now_s() - t0;
+    return count;
+}
+
+// ---- streaming write path ---------------------------------------------------
+
+int Engine::write_begin() {
+    HIP_TRY(hipSetDevice(device_));
+    int rc = ensure_ring();
+    if (rc) return rc;
+    // A window holds the carried chunk (<= max bytes) at offset 0, then the
+    // new bytes: its start stays 16-byte aligned for the scan's vector loads.
+    const size_t reserve = round_up(std::max(max_, min_) + 16, 256);  // FSChunker: max_ = 0
+    if (!ws_win_[0]) {
+        for (auto &w : ws_win_) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&w), reserve + kWriteWindow + 64));
+        HIP_TRY(hipEventCreateWithFlags(&ws_ev_, hipEventDisableTiming));
+    }
+    wr_ = WriteState{};
+    wr_.reserve = reserve;
+    wr_.active = true;
+    wr_.t0 = now_s();
+    return CDC_OK;
+}
+
+// Chunk the current window [0, carry + fill) on the device;
+// all chunks but the last (all of them at the end of the write) are spans.
+int Engine::write_window(bool final) {
+    WriteState &W = wr_;
+    const size_t n = W.carry + W.fill;
+    if (n == 0) return CDC_OK;
+    uint8_t *base = ws_win_[W.cur];
+    // The window's uploads ran on the copy stream: the chunking waits for them.
+    HIP_TRY(hipEventRecord(copy_done_, copy_stream_));
+    HIP_TRY(hipStreamWaitEvent(own_stream_, copy_done_, 0));
+    const size_t need = max_chunks(n);
+    int rc = ensure_host_out(need);
+    if (rc) return rc;
+    const uint8_t *p = base;
+    const uint64_t l = n;
+    uint64_t first[2] = {0, 0};
+    const double tc = now_s();
+    const int64_t c = chunk_batch_device(1, &p, &l, reinterpret_cast<cdc_chunk_t *>(d_hout_), need, first,
+                                         own_stream_);
+    if (c < 0) return (int)c;
+    W.chunk_s += now_s() - tc;
+    const cdc_chunk_t *ch = h_out_;
+    const int64_t keep = final ? c : c - 1;
+    for (int64_t i = 0; i < keep; ++i) W.spans.push_back(ch[i].length);
+    if (!final && c > 0) {
+        // storage.rs:322: the last chunk is carried (`rest`), here in HBM, to the
+        // front of the other window (it is <= max bytes: the reserve).
+        const size_t r = (size_t)ch[c - 1].length;
+        uint8_t *dst = ws_win_[1 - W.cur];
+        HIP_TRY(hipMemcpyAsync(dst, base + ch[c - 1].offset, r, hipMemcpyDeviceToDevice, own_stream_));
+        // new uploads into that window wait for the carry copy (same region's
+        // neighbourhood; cheap)
+        HIP_TRY(hipEventRecord(ws_ev_, own_stream_));
+        HIP_TRY(hipStreamWaitEvent(copy_stream_, ws_ev_, 0));
+        W.carry = r;
+    } else {
+        W.carry = 0;
+    }
+    W.cur = 1 - W.cur;
+    W.fill = 0;
+    return CDC_OK;
+}
+
+int Engine::write_segment(const uint8_t *data, size_t len) {
+    if (!wr_.active) {
+        set_error("cdc_write_segment: no write in progress (cdc_write_begin)");
+        return CDC_EINVAL;
+    }
+    if (len && !data) {
+        set_error("cdc_write_segment: data is NULL");
+        return CDC_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    WriteState &W = wr_;
+    while (len) {
+        if (W.fill == kWriteWindow) {
+            const int rc = write_window(false);
+            if (rc) return rc;
+        }
+        const size_t n = std::min(len, kWriteWindow - W.fill);
+        const int rc = upload(data, n, ws_win_[W.cur] + W.carry + W.fill, copy_stream_, kRingSlot);
+        if (rc) return rc;
+        W.fill += n;
+        W.bytes += n;
+        data += n;
+        len -= n;
+    }
+    W.segments += 1;
+    return CDC_OK;
+}
+
+int64_t Engine::write_finish(std::vector<uint64_t> &spans, double *seconds) {
+    if (!wr_.active) {
+        set_error("cdc_write_finish: no write in progress (cdc_write_begin)");
+        return CDC_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    const int rc = write_window(true);  // StorageWriter::flush: the rest is the last span
+    wr_.active = false;
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(copy_stream_));
+    spans.swap(wr_.spans);
+    if (seconds) *seconds = now_s() - wr_.t0;
+    return (int64_t)spans.size();
+}
+
+int Engine::host_stats(double *v, size_t n) const {
+    const double s[5] = {(double)host_.calls, host_.upload_s, host_.total_s, wr_.chunk_s, (double)wr_.segments};
+    for (size_t i = 0; i < n && i < 5; ++i) v[i] = s[i];
+    return CDC_OK;
+}
+
+}  // namespace cdc

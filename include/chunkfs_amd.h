@@ -159,20 +159,35 @@ typedef struct cdc_timing {
  * never overrun when fields are appended in a later version. */
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size);
 
-/* ---- Write path mirror --------------------------------
+/* ---- Write path ---------------------------------------
  * ChunkStorage::write (storage.rs:78-103) + StorageWriter::{write,flush}
- * (storage.rs:302-383) for ONE write call: seg_size (1 MiB) slices, carry-over
- * of the last chunk of every segment, flush of the rest.  Writes the span
- * lengths in file order (min(count, cap) of them) and returns the span count.
- * FastCDC and fixed-size chunking restart at every chunk boundary, so the
- * spans do not depend on seg_size (> 0): the library uploads the write once
- * and chunks it in device windows of up to 4 GiB with the same carry-over.
- * *chunk_seconds (may be NULL) receives the wall time of the whole call
- * (H2D + chunking + D2H), the device path's counterpart of the reference's
- * summed chunk_data time (storage.rs:314-316). */
+ * (storage.rs:302-383) for ONE write call: seg_size slices (1 MiB in the
+ * reference), carry-over of the last chunk of every segment, flush of the
+ * rest.  Writes the span lengths in file order (min(count, cap) of them) and
+ * returns the span count.  Runs the streaming path below with seg_size
+ * segments.  *chunk_seconds (may be NULL) receives the wall time of the whole
+ * call (host copy into pinned memory + H2D + chunking + chunk list), i.e. NOT
+ * the reference's summed chunk_data time (storage.rs:314-316), which excludes
+ * the copies: compare it with the reference's write time. */
 int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
                      size_t seg_size, uint64_t *span_lengths, size_t cap,
                      double *chunk_seconds);
+
+/* Streaming form of the same write (ChunkStorage::write_from_stream,
+ * storage.rs:105-137: segments of any size, short reads included): begin,
+ * then one cdc_write_segment per StorageWriter::write, then finish (=
+ * StorageWriter::flush) returns the spans exactly as the reference's loop over
+ * the same segments would.  A segment is copied into a handle-owned pinned
+ * ring and uploaded asynchronously while the caller goes on; the device
+ * chunks 256 MiB windows of the file, carrying each window's last chunk to the
+ * next one in HBM.  The caller's bytes are not retained after a call returns.
+ * One write per handle at a time. */
+int cdc_write_begin(cdc_handle_t *h);
+int cdc_write_segment(cdc_handle_t *h, const uint8_t *data, size_t len);
+/* Span lengths (min(count, cap) written), returns the span count; *seconds
+ * (may be NULL) = wall time since cdc_write_begin. */
+int64_t cdc_write_finish(cdc_handle_t *h, uint64_t *span_lengths, size_t cap,
+                         double *seconds);
 
 /* ---- Chunk fingerprints -------------------------------
  * Sha256Hasher::hash (src/hashers.rs:20-36), applied to every chunk as

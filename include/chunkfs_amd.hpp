@@ -98,6 +98,22 @@ class Chunker {
         return spans;
     }
 
+    // ChunkStorage::write_from_stream (storage.rs:105-137) through the
+    // streaming write path: begin, one write_segment per StorageWriter::write,
+    // finish = flush; returns the span lengths.
+    void write_begin() { check(cdc_write_begin(h_)); }
+    void write_segment(const uint8_t *data, size_t len) {
+        check(cdc_write_segment(h_, data, len));
+        written_ += len;
+    }
+    std::vector<uint64_t> write_finish(double *seconds = nullptr) {
+        std::vector<uint64_t> spans(cdc_max_chunk_count(h_, written_) + 1);
+        written_ = 0;
+        const int64_t n = check(cdc_write_finish(h_, spans.data(), spans.size(), seconds));
+        spans.resize((size_t)n);
+        return spans;
+    }
+
     cdc_handle_t *handle() { return h_; }
 
   protected:
@@ -106,6 +122,7 @@ class Chunker {
         check(cdc_create(algo, (uint32_t)min, (uint32_t)avg, (uint32_t)max, device, &h_));
     }
     cdc_handle_t *h_ = nullptr;
+    size_t written_ = 0;
 };
 
 // FastChunker (src/chunkers/fast.rs): FastCDC 2020, default 8/16/64 KiB.

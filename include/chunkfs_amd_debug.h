@@ -23,6 +23,11 @@ uint32_t cdc_debug_record_cap(const cdc_handle_t *h);
  * hit | bit31 mask_s hit).  Returns the bytes copied or a negative CDC_E*
  * code (CDC_EINVAL for any other `what`). */
 int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes);
+/* Host-path statistics into v[0..n): cdc_chunk_data calls, their upload
+ * seconds (CPU copy into the pinned ring + queueing the H2D), their total
+ * seconds, then the chunking seconds and segment count of the current or
+ * last streaming write (cdc_write_*). */
+int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n);
 
 #ifdef __cplusplus
 }

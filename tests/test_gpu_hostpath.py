@@ -1,0 +1,140 @@
+"""The host-memory boundary on the GPU (-m gpu): cdc_chunk_data through the
+pinned upload ring with the chunk list written into host-mapped memory, and the
+streaming write path (cdc_write_begin / _segment / _finish) against the
+reference's StorageWriter semantics (storage.rs:105-137, 302-383) restated by
+the oracle: for every chunker here the spans of the per-segment loop equal
+the chunks of the whole write, for any segment sizes."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+SIZES = {"fast": (4096, 8192, 16384), "rabin": (2048, 4096, 8192), "ultra": (4096, 8192, 16384),
+         "leap": (4096, 8192, 16384), "seq": (4096, 8192, 16384), "fixed": (4096, 0, 0)}
+
+
+def _chunker(algo):
+    import chunkfs_amd as c
+    s = SIZES[algo]
+    if algo == "fixed":
+        return c.FSChunker(s[0])
+    if algo == "seq":
+        return c.SeqChunker(c.OperationMode.Increasing, c.SizeParams(*s))
+    cls = {"fast": c.FastChunker, "rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}[algo]
+    return cls(c.SizeParams(*s))
+
+
+def _whole(algo, data):
+    s = SIZES[algo]
+    if algo == "fast":
+        return oracle.fastcdc(data, *s)[:, 1]
+    if algo == "fixed":
+        n, cs = data.size, s[0]
+        return np.array([min(cs, n - o) for o in range(0, n, cs)], dtype=np.uint64)
+    return oracle.cdc(algo, data, *s)[:, 1]
+
+
+def _segments(n, rng):
+    """Segment sizes of a write_from_stream: 1 MiB reads with short reads,
+    empty reads and a few large ones."""
+    out, left = [], n
+    while left:
+        r = rng.random()
+        k = 1 << 20 if r < 0.6 else int(rng.integers(0, 5000)) if r < 0.8 else int(rng.integers(1, 9 << 20))
+        k = min(k, left)
+        out.append(k)
+        left -= k
+    return out
+
+
+@pytest.mark.parametrize("algo", ["fast", "rabin", "ultra", "leap", "seq", "fixed"])
+def test_stream_write_matches_storage_writer(algo):
+    import chunkfs_amd as c
+    rng = np.random.default_rng(hash(algo) & 0xFFFF)
+    data = oracle.splitmix64_bytes((40 << 20) + 12345, 77)
+    ch = _chunker(algo)
+    w = c.StreamWriter(ch)
+    off = 0
+    for k in _segments(data.size, rng):
+        w.write(data[off:off + k])
+        off += k
+    spans, secs = w.finish()
+    assert secs > 0
+    ref = _whole(algo, data)
+    assert spans.shape == ref.shape and (spans == ref).all(), algo
+    assert int(spans.sum()) == data.size
+    if algo != "fixed":  # the oracle's own 1 MiB StorageWriter loop agrees too
+        ref_fs, _ = oracle.fs_write(algo, data, *SIZES[algo])
+        assert [int(x) for x in spans] == [int(x) for x in ref_fs]
+    ch.close()
+
+
+def test_stream_write_crosses_device_windows():
+    """600 MiB in 1 MiB segments: the 256 MiB device windows and the carried
+    chunk between them (the reference's `rest`, in HBM here)."""
+    import chunkfs_amd as c
+    data = oracle.splitmix64_bytes(600 << 20, 5)
+    ch = _chunker("fast")
+    w = c.StreamWriter(ch)
+    for off in range(0, data.size, 1 << 20):
+        w.write(data[off:off + (1 << 20)])
+    spans, _ = w.finish()
+    ref = _whole("fast", data)
+    assert spans.shape == ref.shape and (spans == ref).all()
+    st = c.host_stats(ch)
+    assert st["write_segments"] == 600 and st["write_chunk_s"] > 0
+    # the same handle serves a second write (fresh StorageWriter, storage.rs:79)
+    spans2, _ = c.write_spans(ch, data[:3 << 20])
+    ref2 = _whole("fast", data[:3 << 20])
+    assert spans2.shape == ref2.shape and (spans2 == ref2).all()
+    ch.close()
+
+
+def test_stream_write_edge_cases():
+    import chunkfs_amd as c
+    ch = _chunker("fast")
+    w = c.StreamWriter(ch)  # empty write: no span (storage.rs:318-320, 364-366)
+    spans, _ = w.finish()
+    assert spans.size == 0
+    w = c.StreamWriter(ch)
+    for part in (b"", b"abc", b"", b"defgh"):
+        w.write(part)
+    spans, _ = w.finish()
+    assert [int(x) for x in spans] == [8]
+    with pytest.raises(c.CdcError):
+        w.finish()  # no write in progress
+    ch.close()
+
+
+@pytest.mark.parametrize("algo", ["fast", "rabin", "ultra", "leap", "seq", "fixed"])
+def test_chunk_data_pinned_path(algo):
+    """cdc_chunk_data over host buffers of every size class (pieces of the
+    pinned ring, the host-mapped chunk list), unaligned views included."""
+    ch = _chunker(algo)
+    base = oracle.splitmix64_bytes((20 << 20) + 64, 11)
+    for n, off in [(1, 0), (4097, 3), ((1 << 20) + 5, 1), ((8 << 20) + 1, 7), ((20 << 20) + 3, 13)]:
+        data = base[off:off + n]
+        got = ch.chunk_array(data)
+        ref = _whole(algo, np.ascontiguousarray(data))
+        assert got.shape[0] == ref.size and (got[:, 1] == ref).all(), (algo, n)
+        assert int(got[0, 0]) == 0 and (got[1:, 0] == np.cumsum(got[:-1, 1])).all()
+    ch.close()
+
+
+def test_reference_1MiB_loop_through_chunk_data():
+    """The Rust shim's loop (StorageWriter::write per 1 MiB: buffer = rest ++
+    segment, chunk_data, rest = last chunk; flush) through cdc_chunk_data."""
+    data = oracle.splitmix64_bytes((24 << 20) + 999, 123)
+    ch = _chunker("fast")
+    spans, rest = [], np.empty(0, dtype=np.uint8)
+    for off in range(0, data.size, 1 << 20):
+        buf = np.concatenate([rest, data[off:off + (1 << 20)]])
+        chunks = ch.chunk_array(buf)
+        spans += [int(x) for x in chunks[:-1, 1]]
+        o, ln = (int(x) for x in chunks[-1])
+        rest = buf[o:o + ln]
+    spans.append(rest.size)
+    ref, _ = oracle.fs_write("fast", data, *SIZES["fast"])
+    assert spans == [int(x) for x in ref]
+    ch.close()
