@@ -673,6 +673,24 @@ int Engine::init_walk(const uint32_t *seq) {
     wp.bits_fine = 1;
     if (const char *f = std::getenv("CHUNKFS_AMD_BITS_FINE")) wp.bits_fine = std::atoi(f) != 0 ? 1u : 0u;
     wp.cap = (uint32_t)((1ull << seg_log2_) / min_ + 2);
+    // Link mode (Rabin, UltraCDC, LeapCDC): candidate lists of ~4x
+    // the expected count per segment -- Rabin hits 2^-round(log2 avg) per
+    // position, UltraCDC mask_l hits ~2^-11 (Hamming distance 16..19 of 64),
+    // LeapCDC eligible-window runs ~2^-round(log2(avg - min));
+    // CHUNKFS_AMD_LINKS=0 disables.  (SeqCDC's candidates -- completed runs --
+    // are too dense: it keeps direct walks.)
+    // Default on where it measured faster (1 GiB, 4/8/16 KiB: UltraCDC 223 ->
+    // 252 GiB/s; Rabin 573 -> 520 and LeapCDC 153 -> 143 lose).
+    const bool linkable = algo_ == CDC_ALGO_RABIN || algo_ == CDC_ALGO_ULTRA || algo_ == CDC_ALGO_LEAP;
+    wp.links = algo_ == CDC_ALGO_ULTRA ? 1u : 0u;
+    if (const char *l = std::getenv("CHUNKFS_AMD_LINKS")) wp.links = std::atoi(l) != 0 && linkable;
+    {
+        const uint32_t dens = algo_ == CDC_ALGO_RABIN ? cdc_log2_round(avg_) : algo_ == CDC_ALGO_ULTRA ? 10u : lb;
+        const uint64_t expect = ((1ull << seg_log2_) >> dens) + 1;
+        uint64_t cc = 16;
+        while (cc < 4 * expect && cc < 1024) cc <<= 1;
+        wp.ccap = (uint32_t)cc;
+    }
     // Bitmap mode: Rabin when every tested digest is a full
     // window (min >= 48), UltraCDC, LeapCDC, and SeqCDC when its run length
     // fits a 64-bit step (seq_length <= 63).  CHUNKFS_AMD_WALK_BYTES=1 forces
@@ -682,6 +700,7 @@ int Engine::init_walk(const uint32_t *seq) {
            : (wp.seq_len <= 63 ? 1u : 0u);
     if (const char *b = std::getenv("CHUNKFS_AMD_WALK_BYTES"))
         if (std::atoi(b) != 0) wp.nbm = 0;
+    if (!wp.nbm) wp.links = 0;  // links are computed over the bitmaps
     wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);
     wp.bm = nullptr;
     // Tables: Rabin mod/out (appending a byte; sliding one out of the window),
@@ -718,6 +737,11 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
     const size_t oF = take((N + 1) * 8), oG = take((4 + 4 * walk::kMaxFixRounds) * 8);
     const size_t oBM = take(S * (size_t)wp_.seg_words * wp_.nbm * 8);  // predicate bitmaps
+    const size_t cc = wp_.links ? wp_.ccap : 0;                          // link mode
+    const size_t oCN = take(S * 4), oCP = take(S * cc * 4), oLN = take(S * cc * 8), oLI = take(S * cc * 4);
+    const size_t vc = wp_.links ? S * 8 : 0;
+    const size_t oVC = take((2 * walk::kVirtRounds + 2) * 8), oVP = take(vc * 8), oVS = take(vc * 4),
+                 oVN = take(vc * 8), oVI = take(vc * 4);
     const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
     (void)hipFree(wws_);
     wws_ = nullptr;
@@ -739,6 +763,16 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wst_.first = reinterpret_cast<uint64_t *>(b + oF);
     wst_.flags = reinterpret_cast<unsigned long long *>(b + oG);
     wp_.bm = wp_.nbm ? reinterpret_cast<uint64_t *>(b + oBM) : nullptr;
+    wp_.ccnt = reinterpret_cast<uint32_t *>(b + oCN);
+    wp_.cpos = reinterpret_cast<uint32_t *>(b + oCP);
+    wp_.lnext = reinterpret_cast<uint64_t *>(b + oLN);
+    wp_.lidx = reinterpret_cast<uint32_t *>(b + oLI);
+    wp_.vcap = (uint32_t)vc;
+    wp_.vcnt = reinterpret_cast<unsigned long long *>(b + oVC);
+    wp_.vpos = reinterpret_cast<uint64_t *>(b + oVP);
+    wp_.vseg = reinterpret_cast<uint32_t *>(b + oVS);
+    wp_.vnext = reinterpret_cast<uint64_t *>(b + oVN);
+    wp_.vidx = reinterpret_cast<uint32_t *>(b + oVI);
     d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
     d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
     d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
@@ -751,8 +785,37 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     uint64_t *h_first = h_flags + 4;
     HIP_TRY(hipMemsetAsync(wst_.flags, 0, 4 * 8, s));
     HIP_TRY(hipEventRecord(ev_[0], s));
+    static const bool diag = std::getenv("CHUNKFS_AMD_WALKDIAG") != nullptr;  // phase times + candidates
+    auto lap = [&](const char *what) -> int {
+        if (!diag) return CDC_OK;
+        static auto t_last = std::chrono::steady_clock::now();
+        HIP_TRY(hipStreamSynchronize(s));
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "  walkdiag %-6s %9.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+        return CDC_OK;
+    };
+    (void)lap("start");
     HIP_TRY(walk::launch_bits(st, wp_, s));
+    (void)lap("bits");
+    HIP_TRY(walk::launch_links(st, wp_, s));
+    (void)lap("links");
+    if (diag && wp_.links) {
+        std::vector<uint32_t> cn(st.total_spans);
+        HIP_TRY(hipMemcpy(cn.data(), wp_.ccnt, cn.size() * 4, hipMemcpyDeviceToHost));
+        uint64_t tot = 0, ovf = 0, mx = 0;
+        for (uint32_t c : cn) {
+            tot += c;
+            ovf += c > wp_.ccap;
+            mx = c > mx ? c : mx;
+        }
+        std::fprintf(stderr, "  walkdiag candidates %llu (%.2f per segment, max %llu, cap %u, overflowed %llu of %zu)\n",
+                     (unsigned long long)tot, (double)tot / cn.size(), (unsigned long long)mx, wp_.ccap,
+                     (unsigned long long)ovf, cn.size());
+    }
     HIP_TRY(walk::launch_walk(st, wp_, wst_, s));
+    (void)lap("walk");
     HIP_TRY(hipEventRecord(ev_[1], s));
     // Jacobi rounds: re-walk every segment whose entry is not its predecessor's
     // exit, until none is.  Rounds are launched in groups without a host sync:
@@ -778,7 +841,13 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
             walk::WalkState ws = wst_;
             ws.flags = rf + 4 * r;
             ws.gate = r ? rf + 4 * (r - 1) : nullptr;
+            const auto t0 = std::chrono::steady_clock::now();
             HIP_TRY(walk::launch_fix(st, wp_, ws, s));
+            if (diag) {
+                HIP_TRY(hipStreamSynchronize(s));
+                std::fprintf(stderr, "  walkdiag round %u %.3f ms\n", r,
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+            }
         }
         launched = end;
         HIP_TRY(hipMemcpyAsync(h_rf, rf, (size_t)launched * 4 * 8, hipMemcpyDeviceToHost, s));
@@ -789,12 +858,19 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         round_errors += h_rf[4 * r + 1];
         rewalked += h_rf[4 * r + 3];
     }
+    if (diag) {
+        std::fprintf(stderr, "  walkdiag rounds %u settled %d:", launched, (int)settled);
+        for (uint32_t r = 0; r < launched && r < 24; ++r)
+            std::fprintf(stderr, " %llu/%llu", (unsigned long long)h_rf[4 * r + 3], (unsigned long long)h_rf[4 * r]);
+        std::fprintf(stderr, "\n");
+    }
     // Chains that never merge (periodic data): one exact in-order pass from
     // the lowest segment the last round changed.
     if (!settled) {
         HIP_TRY(hipMemcpyAsync(wst_.flags + 2, rf + 4 * (R - 1) + 2, 8, hipMemcpyDeviceToDevice, s));
         HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
     }
+    (void)lap("fixup");
     HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
     HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));

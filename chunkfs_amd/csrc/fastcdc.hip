@@ -36,6 +36,9 @@ namespace {
 
 // ---- common helpers --------------------------------------------------------
 
+// Candidate record (u32): span offset (bits 0-23) | truncated-region result of
+// a chunk starting there (bits 24-29, written by the scan's flush; 62 =
+// unknown) | mask_l hit (30) | mask_s hit (31).
 constexpr uint32_t kCandPosMask = 0x00FFFFFFu;
 constexpr uint32_t kCandHitL = 1u << 30;
 constexpr uint32_t kCandHitS = 1u << 31;
@@ -66,6 +69,9 @@ __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
 #endif
 #ifndef CDC_SCAN_LOOK
 #define CDC_SCAN_LOOK 1
+#endif
+#ifndef CDC_SCAN_TRUNC
+#define CDC_SCAN_TRUNC 0
 #endif
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -128,6 +134,8 @@ __device__ __forceinline__ uint64_t gear_prefix(uint64_t g, uint32_t lane) {
 
 constexpr uint32_t kTruncMax = 47;    // mask bits <= 47 (checked on the host)
 constexpr uint32_t kTruncNone = 63;   // truncated-region result: no hit
+constexpr uint32_t kTruncUnknown = 62;  // record field: not precomputed (near the stream end)
+constexpr int kRecTShift = 24;        // record bits 24..29: the record's truncated-region result
 
 struct Regime {
     uint64_t rem, a0, ce, re, tl;
@@ -342,11 +350,61 @@ __device__ __forceinline__ void stage_step(Q4 &C, const Q4 &X, uint4 *wrow, cons
     __builtin_amdgcn_wave_barrier();
 }
 
+// The resolve's per-record work, done here while the bytes stream by: the
+// truncated-region result of a chunk starting at span offset c (first d in
+// [0, trunc) whose in-chunk hash, reset at c + a0, hits mask_s below the
+// centre / mask_l above it; kTruncNone if none) -- for chunks whose regime is
+// the steady one (>= max bytes to the stream end), else kTruncUnknown.  The
+// 52 bytes come as 13 dword loads realigned with v_alignbyte_b32; the table is
+// the scan's pre-shifted one, so the masks are the shifted ones.
+typedef const __attribute__((address_space(3))) uint64_t lds_u64;
+typedef const __attribute__((address_space(3))) char lds_char;
+
+#if CDC_SCAN_TRUNC
+// Out of line (keeps the scan loop's registers free); the table pointer is
+// an explicit LDS one so that the lookups stay ds_read_b64.
+__device__ __noinline__ uint32_t scan_trunc(const uint8_t *base, uint32_t c, uint64_t avail, lds_u64 *ltab,
+                                            uint32_t rep, uint32_t mn, uint32_t avg, uint32_t mx, uint32_t trunc,
+                                            uint64_t mask_s, uint64_t mask_l) {
+    const uint32_t a0 = (mn / 2) * 2, ce = (avg / 2) * 2, re = (mx / 2) * 2;
+    if (avail - c < (uint64_t)mx || (uint64_t)a0 + 52 > avail - c) return kTruncUnknown;
+    const uint32_t tl = min(a0 + trunc, re);
+    if (tl <= a0) return kTruncNone;
+    const uint32_t len = tl - a0;
+    const uint64_t w0 = (uint64_t)c + a0;
+    const uint64_t al = w0 & ~3ull;
+    const uint32_t sh = (uint32_t)(w0 - al);
+    uint32_t w[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(base + al + 4 * i);
+    uint64_t h = 0;
+    uint32_t t = kTruncNone;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const uint32_t a = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t d = 4 * k + j;
+            if (d >= kTruncMax) break;
+            const uint32_t addr = __builtin_amdgcn_perm(rep, a, 0x0c0c0004u | ((uint32_t)j << 8));
+            h = shl1_add(h, *reinterpret_cast<lds_u64 *>(reinterpret_cast<lds_char *>(ltab) + addr));
+            const bool hit = d < len && !(h & ((a0 + d) < ce ? mask_s : mask_l));
+            t = (hit && t == kTruncNone) ? d : t;
+        }
+    }
+    return t;
+}
+
+#endif
+
 // Flush of one span: exact mask_s / mask_l flags for each hitting quarter
-// (re-hashed from the hash before it), position order, HBM write.
-__device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint32_t span_len, uint32_t sub_mask,
-                                           uint32_t ne, const EntryList &E, const uint64_t *tab, uint32_t rep,
-                                           const FastParams &fp, const Candidates &cand, uint32_t lane) {
+// (re-hashed from the hash before it), each record's truncated-region result
+// (scan_trunc), position order, HBM write.  avail = stream bytes from the span
+// start.
+__device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint32_t span_len, uint64_t avail,
+                                           uint32_t sub_mask, uint32_t ne, const EntryList &E, const uint64_t *tab,
+                                           uint32_t rep, const FastParams &fp, const Candidates &cand,
+                                           uint32_t lane) {
     wave_sync_lds();
     uint32_t *cpos = cand.pos + g * cand.cap;
     if (ne > kEntCap) {  // too many hits for the LDS list: resolve takes the exact slow path
@@ -389,8 +447,17 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
     if (keep) {
         for (uint32_t m = hs | hl; m; m &= m - 1) {
             const uint32_t j = __builtin_ctz(m);
+            // (bits 24-29: kTruncUnknown.  Precomputing the record's truncated
+            // result here -- scan_trunc -- took 10 us off the resolve's link
+            // pass but added 17 us of VALU to the scan: off by default,
+            // CDC_SCAN_TRUNC=1 in an experiment build.)
+            uint32_t t = kTruncUnknown;
+#if CDC_SCAN_TRUNC
+            t = scan_trunc(base, my_pos + j, avail, (lds_u64 *)tab, rep, fp.min, fp.avg, fp.max, fp.trunc,
+                           fp.mask_s_sh, fp.mask_l_sh);
+#endif
             if (slot < cand.cap)
-                cpos[slot] = (my_pos + j) | (((hs >> j) & 1u) << 31) | (((hl >> j) & 1u) << 30);
+                cpos[slot] = (my_pos + j) | (t << kRecTShift) | (((hs >> j) & 1u) << 31) | (((hl >> j) & 1u) << 30);
             ++slot;
         }
     }
@@ -511,6 +578,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
 #undef CDC_PROC
         // This span's carry-in bytes and identity, then the next span's prefetch.
         const uint64_t g_cur = g, off_cur = off;
+        const uint64_t avail_cur = st.lens[si] - off;
         const uint32_t wb_cur = wb;
         const uint8_t *base_cur = base;
         g = next_full(g + gstride, si, off);
@@ -527,7 +595,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
             h0 = h;
             append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, (lo + 32) | kEntFix, h0, ne, E);
         }
-        flush_span(g_cur, base_cur, (uint32_t)span, sub - 1, ne, E, tab, rep, fp, cand, lane);
+        flush_span(g_cur, base_cur, (uint32_t)span, avail_cur, sub - 1, ne, E, tab, rep, fp, cand, lane);
     }
 }
 
@@ -569,7 +637,7 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
         if (active && p < span_len) hit = quarter<kAlign>(h, ld16_guarded(base, p, span_len), tab, rep, fp) == 0;
         append_hits(hit, p | kEntFix, h0, ne, E);
     }
-    flush_span(g, base, span_len, 0, ne, E, tab, rep, fp, cand, lane);
+    flush_span(g, base, span_len, span_len, 0, ne, E, tab, rep, fp, cand, lane);
 }
 
 
@@ -584,8 +652,6 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 
 constexpr int kResWaves = 4;
 constexpr int kResThreads = kResWaves * 64;
-
-typedef const __attribute__((address_space(3))) uint64_t lds_u64;
 
 // First hitting offset d in [0, tl-a0) of the truncated positions of the
 // chunk starting at c (hash reset at c+a0), or kTruncNone; w0 = c + a0.
@@ -644,17 +710,6 @@ __device__ __noinline__ uint32_t trunc_at(const uint8_t *data, uint64_t n, uint6
 __device__ __forceinline__ uint32_t trunc_call(const uint8_t *data, uint64_t n, uint64_t c, const FastParams &fp,
                                                const uint64_t *tab) {
     return trunc_at(data, n, c, fp.mask_s, fp.mask_l, fp.min, fp.avg, fp.max, fp.trunc, (lds_u64 *)tab);
-}
-
-// Inlined form for the per-record batch (the hot caller).
-__device__ __forceinline__ uint32_t trunc_bytes(const uint8_t *data, uint64_t n, uint64_t c, const FastParams &fp,
-                                                const uint64_t *tab) {
-    if (n - c <= fp.min) return kTruncNone;
-    const Regime R = regime(fp, c, n);
-    if (R.tl <= R.a0) return kTruncNone;
-    const uint64_t w0 = c + R.a0;
-    if ((w0 & ~3ull) + 52 > n) return trunc_call(data, n, c, fp, tab);
-    return trunc_words(data, w0, (uint32_t)(R.tl - R.a0), R.a0, R.ce, fp.mask_s, fp.mask_l, (lds_u64 *)tab);
 }
 
 // Exact next start from the bytes alone, wave-cooperative (64 positions per
@@ -994,6 +1049,7 @@ struct LinkItem {
     bool act, fast;
     int j;
     uint32_t e, i0, si, len;
+    uint32_t known;  // the record's precomputed truncated result, or kTruncUnknown
     uint64_t c, n, a0, ce, w0;
     const uint8_t *data;
 };
@@ -1001,6 +1057,7 @@ struct LinkItem {
 __device__ __forceinline__ LinkItem link_item(const ChainWin &W, const FastParams &fp, bool virt, uint32_t x,
                                               uint32_t e1) {
     LinkItem it{};
+    it.known = kTruncUnknown;
     it.act = x < e1;
     if (!it.act) return it;
     if (virt) {
@@ -1013,6 +1070,7 @@ __device__ __forceinline__ LinkItem link_item(const ChainWin &W, const FastParam
         it.j = W.rslot[x];
         it.c = W.key[x] & kKeyPos;
         it.i0 = x + 1;
+        it.known = (W.rec[x] >> kRecTShift) & 63u;
     }
     it.si = W.ssi[it.j];
     it.n = W.slen[it.j];
@@ -1024,7 +1082,7 @@ __device__ __forceinline__ LinkItem link_item(const ChainWin &W, const FastParam
             it.a0 = R.a0;
             it.ce = R.ce;
             it.w0 = it.c + R.a0;
-            it.fast = (it.w0 & ~3ull) + 52 <= it.n;
+            it.fast = (it.w0 & ~3ull) + 52 <= it.n && it.known == kTruncUnknown;
         }
     }
     return it;
@@ -1034,6 +1092,7 @@ __device__ __forceinline__ LinkItem link_item(const ChainWin &W, const FastParam
 // `safe` when it has none in reach).  (Four 16-byte loads plus a select
 // realignment measured slower: the extra registers cost occupancy.)
 __device__ __forceinline__ void item_load(const LinkItem &it, const void *safe, uint32_t (&w)[13]) {
+    if (!__ballot(it.fast)) return;  // records carry the scan's result: no bytes needed (w unused)
     const uint8_t *src = it.fast ? it.data + (it.w0 & ~3ull) : static_cast<const uint8_t *>(safe);
 #pragma unroll
     for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(src + 4 * i);
@@ -1042,6 +1101,7 @@ __device__ __forceinline__ void item_load(const LinkItem &it, const void *safe, 
 __device__ __forceinline__ uint32_t item_trunc(const LinkItem &it, const uint32_t (&w)[13], const FastParams &fp,
                                                const uint64_t *tab) {
     if (!it.act || it.len == 0) return kTruncNone;
+    if (it.known != kTruncUnknown) return it.known;  // from the scan's flush
     if (!it.fast) return trunc_call(it.data, it.n, it.c, fp, tab);
     const uint32_t r = (uint32_t)(it.w0 & 3);
     uint64_t h = 0;
@@ -1125,53 +1185,103 @@ __device__ __forceinline__ bool wait_final(const Resolve &rs, uint64_t j) {
 }
 
 // Exclusive chunk-count prefix of block b >= 1 (wave 0): walks back over the
-// predecessors' descriptors, 64 per step, to the nearest final (inclusive)
+// predecessors' descriptors, kLbGroups x 64 per step (every lane polls
+// kLbGroups of them, all loads of a step in flight together: one round trip
+// for the statuses, one for the payloads), to the nearest final (inclusive)
 // one, checking every block boundary on the way (exit of block j == entry of
-// block j+1, unless j+1 starts a stream).  Returns 1 with acc = the prefix
-// when this block's entry Eb holds; 0 with acc = the predecessor's inclusive
-// count and pred = its final exit when this block must re-walk from pred;
-// -1 on a poll timeout.
+// block j+1, unless j+1 starts a stream).  Item i of a step is predecessor
+// j0 - i, i = lane + 64 k.  Returns 1 with acc = the prefix when this block's
+// entry Eb holds; 0 with acc = the predecessor's inclusive count and pred =
+// its final exit when this block must re-walk from pred; -1 on a poll
+// timeout.  (64 per step made the last of 512 blocks per GiB take 8 steps.)
+constexpr int kLbGroups = 4;
+
 __device__ int lookback(const Resolve &rs, uint64_t b, uint64_t Eb, uint32_t lane, uint64_t &acc, uint64_t &pred) {
     const uint64_t agg_w = (rs.gen << 2) | kAgg, inc_w = (rs.gen << 2) | kInc;
     for (uint32_t attempt = 0; attempt < 1024; ++attempt) {  // each retry follows a stale block going final
         acc = 0;
-        uint64_t expect = Eb;  // entry of the block after this step's lane-0 block
+        uint64_t expect = Eb;  // entry of the block after this step's item 0
         int64_t j0 = (int64_t)b - 1;
         int64_t stale = -1;
         for (;;) {
-            const int64_t j = j0 - (int64_t)lane;
-            uint64_t w = j >= 0 ? 0 : inc_w;
-            uint64_t mi = 0;
-            uint32_t lim = 63;
+            int64_t j[kLbGroups];
+            uint64_t w[kLbGroups];
+#pragma unroll
+            for (int k = 0; k < kLbGroups; ++k) {
+                j[k] = j0 - (int64_t)lane - 64 * k;
+                w[k] = j[k] >= 0 ? 0 : inc_w;
+            }
+            // lim = first item (in distance order) whose status is final; every
+            // item up to it must be published (aggregate or final).
+            int kl = kLbGroups - 1;
+            uint32_t ll = 63;
+            uint64_t mi[kLbGroups];
             for (uint32_t spins = 0;; ++spins) {
-                if (w != agg_w && w != inc_w) w = ld_agent(&rs.dstat[j]);
-                mi = __ballot(w == inc_w);
-                const uint64_t mp = __ballot(w == agg_w || w == inc_w);
-                lim = mi ? (uint32_t)__ffsll((long long)mi) - 1 : 63u;
-                const uint64_t need = lim == 63 ? ~0ull : (2ull << lim) - 1;
-                if ((mp & need) == need) break;
+#pragma unroll
+                for (int k = 0; k < kLbGroups; ++k)
+                    if (w[k] != agg_w && w[k] != inc_w) w[k] = ld_agent(&rs.dstat[j[k]]);
+                bool ready = true, found = false;
+#pragma unroll
+                for (int k = 0; k < kLbGroups; ++k) {
+                    mi[k] = __ballot(w[k] == inc_w);
+                    const uint64_t mp = __ballot(w[k] == agg_w || w[k] == inc_w);
+                    if (found) continue;
+                    if (mi[k]) {
+                        found = true;
+                        kl = k;
+                        ll = (uint32_t)__ffsll((long long)mi[k]) - 1;
+                        const uint64_t need = (2ull << ll) - 1;
+                        if ((mp & need) != need) ready = false;
+                    } else if (mp != ~0ull) {
+                        ready = false;
+                    }
+                }
+                if (!found) {
+                    kl = kLbGroups - 1;
+                    ll = 63;
+                }
+                if (ready) break;
                 if (spins >= kSpinMax) return -1;
                 __builtin_amdgcn_s_sleep(2);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: loads stay below)
-            const bool inc = w == inc_w;
-            uint64_t cnt = 0, E = kNoDep, X = 0;
-            if (j >= 0 && lane <= lim) {
-                cnt = ld_agent(inc ? &rs.dinc[j] : &rs.dagg[j]);
-                X = ld_agent(inc ? &rs.dXi[j] : &rs.dXa[j]);
-                if (!inc) E = ld_agent(&rs.dE[j]);
+            uint64_t cnt[kLbGroups], E[kLbGroups], X[kLbGroups];
+#pragma unroll
+            for (int k = 0; k < kLbGroups; ++k) {
+                const bool in = k < kl || (k == kl && lane <= ll);
+                const bool inc = w[k] == inc_w;
+                cnt[k] = 0;
+                E[k] = kNoDep;
+                X[k] = 0;
+                if (j[k] >= 0 && in) {
+                    cnt[k] = ld_agent(inc ? &rs.dinc[j[k]] : &rs.dagg[j[k]]);
+                    X[k] = ld_agent(inc ? &rs.dXi[j[k]] : &rs.dXa[j[k]]);
+                    if (!inc) E[k] = ld_agent(&rs.dE[j[k]]);
+                }
             }
-            uint64_t En = __shfl_up(E, 1);
-            if (lane == 0) En = expect;
-            const uint64_t mb = __ballot(lane <= lim && En != kNoDep && X != En);
-            if (mb) {
-                stale = j0 - (int64_t)(__ffsll((long long)mb) - 1) + 1;  // the block whose entry is stale
+            // boundary checks in distance order: item i's exit vs item i-1's entry
+            int64_t bad = -1;
+#pragma unroll
+            for (int k = 0; k < kLbGroups; ++k) {
+                if (k > kl) break;
+                uint64_t En = __shfl_up(E[k], 1);
+                if (lane == 0) En = k == 0 ? expect : readlane_u64(E[k - 1], 63);
+                const bool in = k < kl || lane <= ll;
+                const uint64_t mb = __ballot(in && En != kNoDep && X[k] != En);
+                if (mb && bad < 0) bad = 64 * k + (__ffsll((long long)mb) - 1);
+            }
+            if (bad >= 0) {
+                stale = j0 - bad + 1;  // the block whose entry is stale
                 break;
             }
-            acc += wave_sum(lane <= lim ? cnt : 0);
-            if (mi) return 1;
-            expect = readlane_u64(E, 63);
-            j0 -= 64;
+            uint64_t part = 0;
+#pragma unroll
+            for (int k = 0; k < kLbGroups; ++k)
+                if (k < kl || (k == kl && lane <= ll)) part += cnt[k];
+            acc += wave_sum(part);
+            if (mi[kl]) return 1;  // a final descriptor was reached (item ll of group kl)
+            expect = readlane_u64(E[kLbGroups - 1], 63);
+            j0 -= 64 * kLbGroups;
         }
         if (stale == (int64_t)b) {  // this block's own entry: the predecessor's final exit decides
             if (!wait_final(rs, b - 1)) return -1;

@@ -137,6 +137,52 @@ struct Reader {
     }
 };
 
+// Bitmap reader straight from global memory (L1 / L2), for the link kernels'
+// one-chunk walks: an aligned window of 8 words (4 x 16-byte loads issued
+// together) stays in registers.  Same interface as Reader's bitmap
+// accessors; words past the end read 0.
+struct GReader {
+    const uint64_t *w;
+    uint64_t nw;              // words of the stream's bitmaps
+    uint64_t ck = ~0ull;      // first word of the cached window (multiple of 8)
+    uint64_t c[8];
+
+    __device__ void init(const uint64_t *base, uint64_t nwords) {
+        w = base;
+        nw = nwords;
+        ck = ~0ull;
+    }
+    __device__ __forceinline__ uint64_t word(uint64_t i) {
+        const uint64_t k = i & ~7ull;
+        if (k != ck) {
+            ck = k;
+            if (k + 8 <= nw) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(w + k + 2 * q);
+                    c[2 * q] = ((uint64_t)v.y << 32) | v.x;
+                    c[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) c[q] = k + q < nw ? w[k + q] : 0;
+            }
+        }
+        uint64_t v = c[0];
+#pragma unroll
+        for (int q = 1; q < 8; ++q)
+            if ((i & 7) == (uint64_t)q) v = c[q];
+        return v;
+    }
+    __device__ __forceinline__ uint64_t bits(uint32_t nbm, uint32_t b, uint64_t p, uint32_t n) {
+        const uint64_t k = p >> 6;
+        const uint32_t sh = (uint32_t)(p & 63);
+        uint64_t v = word(k * nbm + b) >> sh;
+        if (sh + n > 64) v |= word((k + 1) * nbm + b) << (64 - sh);
+        return n == 64 ? v : v & ((1ull << n) - 1);
+    }
+};
+
 struct Tabs {
     const uint64_t *mod, *out, *leap;
 };
@@ -249,7 +295,8 @@ __device__ uint64_t cut_seq(Reader &r, uint64_t s, uint64_t n, const WalkParams 
 // ---- the same rules over the predicate bitmaps (bits_kernel) ---------------
 // Rabin (min >= 48): every tested digest is a full 48-byte window, so a hit is
 // the bitmap bit; the cut is the first hit in [s+min-1, s+end-1], plus one.
-__device__ uint64_t cut_rabin_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+template <class R>
+__device__ uint64_t cut_rabin_bits(R &r, uint64_t s, uint64_t n, const WalkParams &wp) {
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
     const uint64_t lo = s + wp.min - 1, hi = s + end - 1;
@@ -265,7 +312,8 @@ __device__ uint64_t cut_rabin_bits(Reader &r, uint64_t s, uint64_t n, const Walk
 // UltraCDC over bitmaps 0 (dist & MASK_S == 0), 1 (dist & MASK_L == 0) and
 // 2 (the 8 bytes at q repeat the 8 before).  64 positions at a time while no
 // block start repeats and no position hits, else block by block as cut_ultra.
-__device__ uint64_t cut_ultra_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+template <class R>
+__device__ uint64_t cut_ultra_bits(R &r, uint64_t s, uint64_t n, const WalkParams &wp) {
     if (n <= wp.min) return n;
     uint64_t normal = wp.avg, end = n;
     if (n >= wp.max) end = wp.max;
@@ -305,7 +353,8 @@ __device__ uint64_t cut_ultra_bits(Reader &r, uint64_t s, uint64_t n, const Walk
 // LeapCDC over bitmaps 0 (primary) and 1 (secondary): the 22 primary windows
 // of candidate c are bits c-22 .. c-1, the failing one nearest to c decides
 // the leap; then the two secondary windows c-23, c-24.
-__device__ uint64_t cut_leap_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+template <class R>
+__device__ uint64_t cut_leap_bits(R &r, uint64_t s, uint64_t n, const WalkParams &wp) {
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
     uint64_t c = wp.min;
@@ -356,7 +405,8 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t z, uint32_t n) {
 // per step: a = positions where a run of seq_len in-sequence pairs completes
 // (the run carried in from the previous step included), tB = the pair at which
 // the opposing count reaches jump_trigger; the earlier event decides.
-__device__ uint64_t cut_seq_bits(Reader &r, uint64_t s, uint64_t n, const WalkParams &wp) {
+template <class R>
+__device__ uint64_t cut_seq_bits(R &r, uint64_t s, uint64_t n, const WalkParams &wp) {
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
     uint32_t cnt = 0, opp = 0;
@@ -403,18 +453,67 @@ __device__ __forceinline__ uint64_t cut(Reader &r, uint64_t s, uint64_t len, con
     }
 }
 
+// Where a walk stands: the stream's first segment (gbase), the segment
+// size, and the candidate slot of the current start (link mode; kNoCand when
+// unknown or not a candidate).
+struct Hop {
+    uint64_t gbase;
+    uint32_t sl2;
+    uint32_t ci;
+};
+
+// Candidate slot of stream offset c (link mode), or kNoCand: a binary search
+// in its segment's ascending list; overflowed segments have no links.
+__device__ __forceinline__ uint32_t find_cand(const WalkParams &wp, const Hop &hp, uint64_t c) {
+    const uint64_t h = hp.gbase + (c >> hp.sl2);
+    const uint32_t n = wp.ccnt[h];
+    if (n > wp.ccap) return kNoCand;
+    const uint32_t *P = wp.cpos + h * wp.ccap;
+    const uint32_t x = (uint32_t)(c & ((1ull << hp.sl2) - 1));
+    uint32_t a = 0, b = n;
+    while (a < b) {
+        const uint32_t m = (a + b) >> 1;
+        if (P[m] < x) a = m + 1; else b = m;
+    }
+    return a < n && P[a] == x ? (uint32_t)(h * wp.ccap + a) : kNoCand;
+}
+
+// The next chunk start after one starting at c: the precomputed link when c
+// is a candidate (link mode), else the rule walked from c.
+template <int kAlgo, bool kBits>
+__device__ __forceinline__ uint64_t advance(Reader &r, uint64_t c, uint64_t len, Hop &hp, const WalkParams &wp,
+                                            const Tabs &T) {
+    if (wp.links && c < len) {
+        if (hp.ci == kNoCand) hp.ci = find_cand(wp, hp, c);
+        if (hp.ci != kNoCand) {
+            uint64_t nx;
+            if (hp.ci & kVirt) {
+                const uint32_t v = hp.ci & ~kVirt;
+                nx = wp.vnext[v];
+                hp.ci = wp.vidx[v];
+            } else {
+                nx = wp.lnext[hp.ci];
+                hp.ci = wp.lidx[hp.ci];
+            }
+            return nx;
+        }
+    }
+    hp.ci = kNoCand;
+    return c + cut<kAlgo, kBits>(r, c, len, wp, T);
+}
+
 // Walk from chunk start c (< seg_end) to the first start >= seg_end,
 // recording the starts in the segment's list.
 template <int kAlgo, bool kBits>
 __device__ void walk_from(uint64_t c, uint64_t g, uint64_t seg_end, uint64_t len, Reader &r,
-                          const WalkParams &wp, const Tabs &T, const WalkState &ws) {
+                          const WalkParams &wp, const Tabs &T, const WalkState &ws, Hop &hp) {
     ws.E[g] = c;
     uint32_t cnt = 0;
     uint64_t *list = ws.list + g * wp.cap;
     while (c < seg_end) {
         if (cnt < wp.cap) list[cnt] = c;
         ++cnt;
-        c += cut<kAlgo, kBits>(r, c, len, wp, T);
+        c = advance<kAlgo, kBits>(r, c, len, hp, wp, T);
     }
     ws.X[g] = c;
     ws.N[g] = cnt;
@@ -431,7 +530,8 @@ constexpr uint32_t kNew = 8;
 
 template <int kAlgo, bool kBits>
 __device__ bool rewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, Reader &r, const WalkParams &wp,
-                       const Tabs &T, const WalkState &ws, uint64_t *nb) {
+                       const Tabs &T, const WalkState &ws, uint64_t *nb, Hop &hp) {
+    hp.ci = kNoCand;
     uint64_t *list = ws.list + g * wp.cap;
     const uint32_t n_old = ws.N[g];
     const uint32_t lim = min(n_old, wp.cap);
@@ -454,7 +554,7 @@ __device__ bool rewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, R
             return false;
         }
         nb[m++] = c;
-        c += cut<kAlgo, kBits>(r, c, len, wp, T);
+        c = advance<kAlgo, kBits>(r, c, len, hp, wp, T);
     }
     if (c >= seg_end) {  // the whole segment in <= kNew starts, no meeting point
         for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
@@ -463,7 +563,8 @@ __device__ bool rewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, R
         ws.X[g] = c;
         return c != x_old;
     }
-    walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws);
+    hp.ci = kNoCand;
+    walk_from<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, hp);
     return ws.X[g] != x_old;
 }
 
@@ -501,15 +602,29 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
     const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
     Reader r;
     init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
+    Hop hp{st.span_base[si], st.span_log2, kNoCand};
     // Warm-up start: `warm` bytes back, on the max-length grid of the stream
-    // (so runs of max-length cuts from the stream start are in phase).
+    // (so runs of max-length cuts from the stream start are in phase); in
+    // link mode the first candidate at or after it, so that the warm-up is a
+    // few hops over links instead of a walk.
     uint64_t c = 0;
     if (off != 0) {
         c = off > wp.warm ? off - wp.warm : 0;
         c = c / wp.max * wp.max;
-        while (c < off) c += cut<kAlgo, kBits>(r, c, len, wp, T);
+        if (wp.links) {
+            const uint64_t h = hp.gbase + (c >> hp.sl2);
+            const uint32_t n = wp.ccnt[h];
+            if (n >= 1 && n <= wp.ccap) {
+                const uint64_t cc = (c & ~((1ull << hp.sl2) - 1)) + wp.cpos[h * wp.ccap];
+                if (cc < off) {
+                    c = cc;
+                    hp.ci = (uint32_t)(h * wp.ccap);
+                }
+            }
+        }
+        while (c < off) c = advance<kAlgo, kBits>(r, c, len, hp, wp, T);
     }
-    walk_from<kAlgo, kBits>(c, g, seg_end, len, r, wp, T, ws);
+    walk_from<kAlgo, kBits>(c, g, seg_end, len, r, wp, T, ws, hp);
 }
 
 // One Jacobi round.  Segment g is scheduled when its entry differs from its
@@ -542,11 +657,12 @@ __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, c
     const uint64_t span = 1ull << st.span_log2;
     Reader r;
     init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
+    Hop hp{st.span_base[si], st.span_log2, kNoCand};
     uint64_t gg = g;
     for (uint32_t k = 0;; ++k) {
         const uint64_t seg_end = min(off + span, len);
         atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
-        if (!rewalk<kAlgo, kBits>(x, gg, seg_end, len, r, wp, T, ws, nbuf + threadIdx.x * kNew)) break;
+        if (!rewalk<kAlgo, kBits>(x, gg, seg_end, len, r, wp, T, ws, nbuf + threadIdx.x * kNew, hp)) break;
         if (seg_end >= len) break;  // the stream's last segment: no successor
         if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
             atomicAdd(&ws.flags[0], 1ull);  // a successor needs another round
@@ -579,7 +695,8 @@ __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
         Reader r;
         init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
-        (void)rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf);
+        Hop hp{st.span_base[si], st.span_log2, kNoCand};
+        (void)rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf, hp);
     }
 }
 
@@ -770,6 +887,158 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     }
 }
 
+// ---- link mode (Rabin, UltraCDC, LeapCDC) ---------------------------------------
+// Candidates: the positions where a chunk can start after a cut that is not a
+// max / end / LEST cut, whatever the previous chunk's start -- so every such
+// cut lands on one:
+//   Rabin  q = p + 1 for a window hit at p (cut_rabin_bits returns i + 1);
+//   Ultra  a mask_s or mask_l hit at q (cut_ultra_bits returns i + j there);
+//   Leap   its 22 primary windows (ending at q-1 .. q-22) and 2 secondary
+//          windows (q-23, q-24) eligible (cut_leap_bits returns c only
+//          then): runs of 22 set bits by doubling over two words.
+// Each lane produces the candidate mask of one 64-position word.
+template <int kAlgo>
+__device__ __forceinline__ uint64_t cand_word(const uint64_t *bm, uint64_t K) {
+    if constexpr (kAlgo == 2) {  // Rabin, one bitmap
+        const uint64_t h1 = bm[K], h0 = K ? bm[K - 1] : 0;
+        return (h1 << 1) | (h0 >> 63);
+    } else if constexpr (kAlgo == 4) {  // Ultra: mask_s | mask_l
+        return bm[K * 3] | bm[K * 3 + 1];
+    } else {  // Leap
+        const uint64_t p1 = bm[K * 2], s1 = bm[K * 2 + 1];
+        const uint64_t p0 = K ? bm[K * 2 - 2] : 0, s0 = K ? bm[K * 2 - 1] : 0;
+        typedef unsigned __int128 u128;
+        const u128 V = ((u128)p1 << 64) | p0, W = ((u128)s1 << 64) | s0;
+        const u128 e2 = V & (V << 1), e4 = e2 & (e2 << 2), e8 = e4 & (e4 << 4), e16 = e8 & (e8 << 8);
+        const u128 e22 = e16 & (e4 << 16) & (e2 << 20);  // bit b: primary bits b-21 .. b all set
+        return (uint64_t)(e22 >> 63) & (uint64_t)(W >> 41) & (uint64_t)(W >> 40);
+    }
+}
+
+template <int kAlgo>
+__global__ __launch_bounds__(kWalkBlock) void cand_kernel(const StreamTable st, const WalkParams wp) {
+    constexpr uint32_t kNbm = kAlgo == 2 ? 1 : kAlgo == 4 ? 3 : 2;
+    // lowest position a cut can reach: min >= 1 (Rabin), >= 8 (Ultra), >= 32 (Leap)
+    constexpr uint64_t kLow = kAlgo == 2 ? 1 : kAlgo == 4 ? 8 : 32;
+    const uint64_t g = blockIdx.x;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint64_t gbase = st.span_base[si];
+    const uint64_t *bm = wp.bm + gbase * (uint64_t)wp.seg_words * kNbm;  // the stream's bitmaps
+    const uint64_t w0 = (off >> 6);                                       // stream word of the segment's start
+    const uint32_t lane = threadIdx.x;
+    uint32_t total = 0;
+    uint32_t *out = wp.cpos + g * wp.ccap;
+    for (uint32_t r = 0; r < wp.seg_words / 64; ++r) {
+        const uint64_t K = w0 + (uint64_t)r * 64 + lane;  // this lane's stream word
+        uint64_t m = 0;
+        if (K * 64 < len) {
+            m = cand_word<kAlgo>(bm, K);
+            const uint64_t q0 = K * 64;  // position of bit 0
+            if (q0 < kLow) m &= ~0ull << (kLow - q0);
+            if (len - q0 < 64) m &= (1ull << (len - q0)) - 1;  // q < len
+        }
+        // ordered compaction: an exclusive prefix of the lanes' counts
+        const uint32_t c = (uint32_t)__popcll(m);
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        uint32_t slot = total + x - c;
+        for (uint64_t mm = m; mm; mm &= mm - 1, ++slot)
+            if (slot < wp.ccap) out[slot] = (uint32_t)(((uint64_t)r * 64 + lane) * 64 + __builtin_ctzll(mm));
+        total += (uint32_t)__shfl(x, 63);
+    }
+    if (lane == 0) wp.ccnt[g] = total;
+}
+
+// The rule's next start after a chunk starting at c, over the global bitmaps.
+template <int kAlgo>
+__device__ __forceinline__ uint64_t link_next(const WalkParams &wp, uint64_t gbase, uint64_t c, uint64_t len) {
+    constexpr uint32_t kNbm = kAlgo == 2 ? 1 : kAlgo == 4 ? 3 : 2;
+    GReader r;
+    r.init(wp.bm + gbase * (uint64_t)wp.seg_words * kNbm, ((len + 63) >> 6) * kNbm);
+    if constexpr (kAlgo == 2) return c + cut_rabin_bits(r, c, len - c, wp);
+    else if constexpr (kAlgo == 4) return c + cut_ultra_bits(r, c, len - c, wp);
+    else return c + cut_leap_bits(r, c, len - c, wp);
+}
+
+// Slot of a link's next start nx: its candidate slot, else a new virtual
+// entry (to be linked by round `round`), else kNoCand (stream end, the
+// budget or the rounds spent: the walk then walks the rule from there).
+__device__ __forceinline__ uint32_t next_slot(const WalkParams &wp, uint32_t sl2, uint64_t gbase, uint64_t nx,
+                                              uint64_t len, uint32_t round) {
+    if (nx >= len) return kNoCand;
+    const Hop hp{gbase, sl2, kNoCand};
+    const uint32_t ci = find_cand(wp, hp, nx);
+    if (ci != kNoCand || round >= kVirtRounds) return ci;
+    const unsigned long long v = atomicAdd(&wp.vcnt[0], 1ull);
+    if (v >= wp.vcap) return kNoCand;
+    wp.vpos[v] = nx;
+    wp.vseg[v] = (uint32_t)gbase;
+    return kVirt | (uint32_t)v;
+}
+
+// Lane per candidate slot (k-major: the 64 lanes of a wave share k, so the
+// waves of high k retire at once): the next chunk start after a chunk
+// starting at the candidate, and that start's slot.
+template <int kAlgo>
+__global__ __launch_bounds__(256) void link_kernel(const StreamTable st, const WalkParams wp) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t S = st.total_spans;
+    const uint64_t k = t / S, g = t - k * S;
+    if (k >= wp.ccap) return;
+    const uint32_t n = wp.ccnt[g];
+    if (n > wp.ccap || k >= n) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint64_t gbase = st.span_base[si];
+    const uint64_t slot = g * wp.ccap + k;
+    const uint64_t nx = link_next<kAlgo>(wp, gbase, off + wp.cpos[slot], len);
+    wp.lnext[slot] = nx;
+    wp.lidx[slot] = next_slot(wp, st.span_log2, gbase, nx, len, 0);
+}
+
+// Round r of the virtual links: the entries allocated before it and after
+// round r-1 started (vcnt[1 + r] .. vcnt[2 + r], snapshots by vmark_kernel).
+template <int kAlgo>
+__global__ __launch_bounds__(256) void vlink_kernel(const StreamTable st, const WalkParams wp, uint32_t round) {
+    const uint64_t v = wp.vcnt[1 + round] + (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t end = min(wp.vcnt[2 + round], (unsigned long long)wp.vcap);
+    if (v >= end) return;
+    const uint64_t gbase = wp.vseg[v];
+    uint32_t si;
+    uint64_t off;
+    locate(st, gbase, si, off);
+    const uint64_t len = st.lens[si];
+    const uint64_t nx = link_next<kAlgo>(wp, gbase, wp.vpos[v], len);
+    wp.vnext[v] = nx;
+    wp.vidx[v] = next_slot(wp, st.span_log2, gbase, nx, len, round + 1);
+}
+
+// Snapshot of the allocation counter: the end of virtual round r.
+__global__ void vmark_kernel(const WalkParams wp, uint32_t round) { wp.vcnt[2 + round] = wp.vcnt[0]; }
+
+template <int kAlgo>
+hipError_t links_dispatch(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(wp.vcnt, 0, (2 * kVirtRounds + 2) * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    cand_kernel<kAlgo><<<(unsigned)st.total_spans, kWalkBlock, 0, s>>>(st, wp);
+    const uint64_t threads = st.total_spans * (uint64_t)wp.ccap;
+    link_kernel<kAlgo><<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(st, wp);
+    for (uint32_t r = 0; r < kVirtRounds; ++r) {  // round r links the entries allocated by round r - 1
+        vmark_kernel<<<1, 1, 0, s>>>(wp, r);
+        vlink_kernel<kAlgo><<<(unsigned)((wp.vcap + 255) / 256), 256, 0, s>>>(st, wp, r);
+    }
+    return hipGetLastError();
+}
+
 // ---- prefix and output -----------------------------------------------------
 
 __device__ __forceinline__ uint64_t block_exclusive(uint64_t v, uint64_t *sh, uint64_t &total) {
@@ -874,6 +1143,14 @@ hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t 
     else if (wp.algo == 6) bits_kernel<6><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
+    if (!st.total_spans || !wp.links) return hipSuccess;
+    if (wp.algo == 2) return links_dispatch<2>(st, wp, s);
+    if (wp.algo == 4) return links_dispatch<4>(st, wp, s);
+    if (wp.algo == 5) return links_dispatch<5>(st, wp, s);
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {

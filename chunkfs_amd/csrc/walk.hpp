@@ -37,7 +37,33 @@ struct WalkParams {
     uint32_t seg_words;       // 64-bit words per segment and bitmap (segment bytes / 64)
     uint32_t bits_fine;       // bitmap pass: lane per 64-position word (Ultra, Leap, Seq)
     uint32_t ahead;           // fix-up round: segments one lane may re-walk (1 = plain Jacobi)
+    // Link mode (LeapCDC): the rule's candidate cut positions (content-defined:
+    // every cut that is not a max / end cut lands on one) are listed per
+    // segment, and the next chunk start after a chunk starting at each of
+    // them is computed once, a lane per candidate (link_kernel); the walks
+    // then hop over links and walk the rule only from other starts.  A
+    // segment with more than ccap candidates (low-entropy data) keeps direct
+    // walks.
+    uint32_t links;           // 1: link mode
+    uint32_t ccap;            // candidates per segment
+    uint32_t *ccnt;           // [S] candidates of each segment (> ccap: overflowed, no links)
+    uint32_t *cpos;           // [S * ccap] their segment offsets, ascending
+    uint64_t *lnext;          // [S * ccap] next chunk start (stream offset) after a chunk starting there
+    uint32_t *lidx;           // [S * ccap] candidate slot of that next start, kVirt | v, or kNoCand
+    // Virtual starts: a link's next start that is not a candidate (a max cut)
+    // gets its own link (vnext / vidx), so that a walk never walks the rule
+    // from a start a link reached; up to kVirtRounds levels deep.
+    uint32_t vcap;            // virtual entries (8 per segment; past it: kNoCand, the walk walks)
+    unsigned long long *vcnt; // [2 * kVirtRounds + 2]: entries allocated, per round: first entry of the round
+    uint64_t *vpos;           // [vcap] stream offset of the virtual start
+    uint32_t *vseg;           // [vcap] its stream's first segment (for find_cand)
+    uint64_t *vnext;          // [vcap] next start after a chunk starting there
+    uint32_t *vidx;           // [vcap] slot of that next start (candidate, kVirt | v, kNoCand)
 };
+
+constexpr uint32_t kNoCand = 0xFFFFFFFFu;
+constexpr uint32_t kVirt = 0x80000000u;
+constexpr uint32_t kVirtRounds = 3;
 
 struct WalkState {
     uint64_t *E;      // [S] entry: first chunk start >= segment start
@@ -61,6 +87,8 @@ constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
 
 // Bitmap mode: the predicate bitmaps of every segment (wave per segment).
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s);
+// Link mode: candidate lists (wave per segment), then the links (lane per candidate).
+hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t s);
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
 // One Jacobi round: snapshot X, then re-walk every segment whose entry is not
 // its predecessor's exit, stopping where the new chain meets the old one.

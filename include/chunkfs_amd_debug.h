@@ -19,8 +19,9 @@ int cdc_debug_pipeline(const cdc_handle_t *h);
 uint32_t cdc_debug_record_cap(const cdc_handle_t *h);
 /* Copy array `what` of the last batch to host memory `out` (at most
  * max_bytes): 0 = per-span candidate counts (u32; > cap means overflowed),
- * 1 = candidate records (u32, cap per span: offset in span | bit30 mask_l
- * hit | bit31 mask_s hit).  Returns the bytes copied or a negative CDC_E*
+ * 1 = candidate records (u32, cap per span: offset in span (bits 0-23) |
+ * truncated-region result of a chunk starting there (bits 24-29; 63 none, 62
+ * not precomputed) | bit30 mask_l hit | bit31 mask_s hit).  Returns the bytes copied or a negative CDC_E*
  * code (CDC_EINVAL for any other `what`). */
 int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes);
 /* Host-path statistics into v[0..n): cdc_chunk_data calls, their upload

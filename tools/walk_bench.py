@@ -3,7 +3,7 @@
 device-resident splitmix64 stream.  CHUNKFS_AMD_WALK="seg_log2,warm_over_max"
 overrides the segment size and warm-up (experiments).  Diagnostics only.
 
-Usage: python3 tools/walk_bench.py [stream_bytes] [min avg max]
+Usage: python3 tools/walk_bench.py [stream_bytes] [min avg max]   (WB_ALGOS=leap,seq selects)
 """
 import ctypes
 import os
@@ -20,7 +20,7 @@ sz = c.SizeParams(*(int(x) for x in sys.argv[2:5])) if len(sys.argv) > 4 else c.
 b = torch.empty(n, dtype=torch.uint8, device="cuda:0")
 _lib.check(_lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, 1, None))
 print("walk", os.environ.get("CHUNKFS_AMD_WALK", "default"), "bytes", n, sz, flush=True)
-for name in ("rabin", "ultra", "leap", "seq"):
+for name in os.environ.get("WB_ALGOS", "rabin,ultra,leap,seq").split(","):
     cls = {"rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}.get(name)
     ch = cls(sz) if cls else c.SeqChunker(0, sz)
     cap = ch.batch_max_chunks([n])
