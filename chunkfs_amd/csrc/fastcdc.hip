@@ -233,6 +233,27 @@ __device__ __forceinline__ void append_hits(bool hit, uint32_t pos, uint64_t h0,
     }
 }
 
+// append_hits that also keeps the quarter's 16 bytes (the DMA scan's flush
+// re-hashes from them instead of re-reading HBM).
+__device__ __forceinline__ void append_hits_d(bool hit, uint32_t pos, uint64_t h0, const uint4 &q, uint32_t &ne,
+                                              const EntryList &E, uint4 *edat) {
+    const uint64_t m = __ballot(hit);
+    if (m) {
+        if (hit) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint32_t slot = ne + below;
+            if (slot < kEntCap) {
+                E.pos[slot] = pos;
+                E.hlo[slot] = (uint32_t)h0;
+                E.hhi[slot] = (uint32_t)(h0 >> 32);
+                edat[slot] = q;
+            }
+        }
+        ne += (uint32_t)__popcll(m);
+    }
+}
+
 // 16 positions of one quarter, the lookups of each dword one dword ahead.
 template <bool kAlign>
 __device__ __forceinline__ uint32_t quarter(uint64_t &h, const uint4 &v, const uint64_t *tab, uint32_t rep,
@@ -324,6 +345,36 @@ __device__ __forceinline__ void process_step(const Q4 &C, uint64_t &h, uint32_t 
     }
 }
 
+// One 64-byte step of a lane for the DMA scan: process_step<kAlign, 1> whose
+// entries keep their quarter's bytes.
+template <bool kAlign>
+__device__ __forceinline__ void process_step_d(const Q4 &C, uint64_t &h, uint32_t pos0, uint32_t &ne,
+                                               const EntryList &E, uint4 *edat, const uint64_t *tab, uint32_t rep,
+                                               const FastParams &fp) {
+    G4 ga, gb;
+    look4(ga, tab, rep, C.q[0].x);
+    SCHED_FENCE();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t h0 = h;
+        uint32_t acc = 0xffffffffu;
+#pragma unroll
+        for (int w = 0; w < 4; w += 2) {
+            look4(gb, tab, rep, word_of(C.q[q], w + 1));
+            SCHED_FENCE();
+            chain4_test<kAlign>(h, acc, ga, fp);
+            SCHED_FENCE();
+            if (q < 3 || w < 2) {
+                look4(ga, tab, rep, w < 2 ? word_of(C.q[q], w + 2) : word_of(C.q[q + 1], 0));
+                SCHED_FENCE();
+            }
+            chain4_test<kAlign>(h, acc, gb, fp);
+            SCHED_FENCE();
+        }
+        append_hits_d(acc == 0, pos0 + 16 * q, h0, C.q[q], ne, E, edat);
+    }
+}
+
 // The 4 coalesced loads of step t: instruction i reads piece (lane%4) of the
 // step of segment 16 i + rsel(lane/4) (16 complete 64-byte pieces per
 // instruction; rsel: see the kernel).
@@ -400,11 +451,11 @@ __device__ __noinline__ uint32_t scan_trunc(const uint8_t *base, uint32_t c, uin
 // Flush of one span: exact mask_s / mask_l flags for each hitting quarter
 // (re-hashed from the hash before it), each record's truncated-region result
 // (scan_trunc), position order, HBM write.  avail = stream bytes from the span
-// start.
+// start.  edat: the entries' bytes in LDS (DMA scan), else re-read from base.
 __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint32_t span_len, uint64_t avail,
                                            uint32_t sub_mask, uint32_t ne, const EntryList &E, const uint64_t *tab,
                                            uint32_t rep, const FastParams &fp, const Candidates &cand,
-                                           uint32_t lane) {
+                                           uint32_t lane, const uint4 *edat = nullptr) {
     wave_sync_lds();
     uint32_t *cpos = cand.pos + g * cand.cap;
     if (ne > kEntCap) {  // too many hits for the LDS list: resolve takes the exact slow path
@@ -421,7 +472,7 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
     if (keep) {
         my_pos = wd & kEntPos;
         uint64_t hh = ((uint64_t)E.hhi[lane] << 32) | E.hlo[lane];
-        const uint4 v = ld16_guarded(base, my_pos, span_len);
+        const uint4 v = edat ? edat[lane] : ld16_guarded(base, my_pos, span_len);
 #pragma unroll
         for (int w = 0; w < 4; ++w)
 #pragma unroll
@@ -597,6 +648,284 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         }
         flush_span(g_cur, base_cur, (uint32_t)span, avail_cur, sub - 1, ne, E, tab, rep, fp, cand, lane);
     }
+}
+
+// ---- scan, LDS-DMA input landing (A/B path: CHUNKFS_AMD_DIAG bit 10) ---------
+//
+// The same scan with the bytes landed by global_load_lds_dwordx4 straight into
+// a per-wave LDS ring: no VGPR staging ring and no ds_write half of the
+// transpose.  DMA instruction i of a step has lane l fetch piece l >> 4 (16
+// bytes) of row 16 i + (l & 15) -- 16 complete 64-byte pieces per instruction,
+// the register path's coalescing -- and lands it lane-linearly, i.e.
+// piece-major inside the instruction's 1 KiB, so lane r reads its 64-byte step
+// with 4 ds_read_b128 whose 16-lane groups hit 16 distinct bank quads
+// (tools/ubench_dma.hip).  Two waves per SIMD (the hashing runs as fast as at
+// four, tools/ubench_hash.hip), two 4 KiB slots per wave: one step in flight
+// while the other is hashed.  Entries keep their quarter's 16 bytes, so the
+// flush re-reads nothing; the 48 carry-in bytes come by one more DMA.  The
+// stream table is read through the constant address space (scalar loads):
+// a vector load would make the compiler drain the untracked DMA with
+// vmcnt(0).  Measured on MI355X (profiles/r03_scan/): bit-exact, but 2-4 %
+// slower than scan_kernel (0.259 vs 0.251 ms per GiB, r03n): with two waves
+// per SIMD the per-span fix-up and flush are not hidden (17 % more VALU than
+// the loop alone, PMC pmc_r03m), so scan_kernel stays the default.
+
+constexpr int kDmaW = 8;
+constexpr uint32_t kDiagDmaScan = 1024;  // CHUNKFS_AMD_DIAG bit 10: this scan instead of scan_kernel (A/B)
+
+struct ScanDmaLds {
+    uint64_t tab[256 * kCopies];   // 64 KiB (LDS address 0)
+    uint4 ring[kDmaW][2][256];     // two 4 KiB step slots per wave
+    uint32_t epos[kDmaW][kEntCap];
+    uint32_t ehlo[kDmaW][kEntCap];
+    uint32_t ehhi[kDmaW][kEntCap];
+    uint32_t ecnt[kDmaW][kEntCap];
+    uint4 edat[kDmaW][kEntCap];    // each entry's 16 bytes
+    uint32_t carry[kDmaW][64];     // the 48 bytes before the next span (DMA, dwords 0..11)
+    uint4 recs[kDmaW][64];         // the span's candidate records, staged for one store
+};
+
+typedef const __attribute__((address_space(4))) uint64_t c_u64;
+typedef const __attribute__((address_space(4))) uint32_t c_u32;
+
+__device__ __forceinline__ uint64_t cld(const uint64_t *p) { return *(c_u64 *)p; }
+
+// One 16-byte piece per lane into LDS at lds_dst + 16 * lane (M0 written in
+// the same statement that reads it; hipcc does not count this load).
+__device__ __forceinline__ void glds16(const uint8_t *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// One dword per lane into LDS at lds_dst + 4 * lane.
+__device__ __forceinline__ void glds4(const uint8_t *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, kCtrl, kRowMask, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), kCtrl, kRowMask, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Sum of v over the wave (mod 2^64), uniform: DPP row_shr 1/2/4/8 leaves each
+// row's total in its lane 15, row_bcast 15/31 carries them into lane 63.
+__device__ __forceinline__ uint64_t wave_total_dpp(uint64_t v) {
+    v += dpp64<0x111, 0xF>(v);
+    v += dpp64<0x112, 0xF>(v);
+    v += dpp64<0x114, 0xF>(v);
+    v += dpp64<0x118, 0xF>(v);
+    v += dpp64<0x142, 0xA>(v);
+    v += dpp64<0x143, 0xC>(v);
+    return readlane_u64(v, 63);
+}
+
+// flush_span for the DMA scan (full spans): the entries' bytes come from LDS,
+// each lane's output slot from a readlane loop over the entries held in
+// registers, and the records are staged in LDS and written with exactly two
+// store instructions (the records, dwordx4 by lanes < cap/4, and the count),
+// so the kernel's DMA waits can count them statically.
+__device__ __forceinline__ void flush_span_d(uint64_t g, uint32_t sub_mask, uint32_t ne, const EntryList &E,
+                                             const uint4 *edat, uint4 *recs, const uint64_t *tab, uint32_t rep,
+                                             const FastParams &fp, const Candidates &cand, uint32_t lane) {
+    wave_sync_lds();
+    uint32_t hs = 0, hl = 0, my_pos = 0xFFFFFFFFu, cnt = 0;
+    const bool ovf = ne > kEntCap;  // too many hits for the LDS list: resolve takes the exact slow path
+    const uint32_t wd = lane < ne && !ovf ? E.pos[lane] : 0u;
+    // (entries of the main loop at a lane's first 48 positions lack the carry-in)
+    const bool keep = lane < ne && !ovf && ((wd & kEntFix) || (wd & sub_mask) >= 48);
+    if (keep) {
+        my_pos = wd & kEntPos;
+        uint64_t hh = ((uint64_t)E.hhi[lane] << 32) | E.hlo[lane];
+        const uint4 v = edat[lane];
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * w + b;
+                hh = (hh << 1) + gear_of(tab, rep, word_of(v, w), b);
+                hs |= (uint32_t)((hh & fp.mask_s_sh) == 0) << j;
+                hl |= (uint32_t)((hh & fp.mask_l_sh) == 0) << j;
+            }
+        cnt = __popc(hs | hl);
+    }
+    uint32_t slot = 0, total = 0;
+    const uint32_t nk = ovf ? 0u : ne;
+    for (uint32_t k = 0; k < nk; ++k) {
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)my_pos, (int)k);
+        const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)k);
+        total += ck;
+        slot += pk < my_pos ? ck : 0u;
+    }
+    uint32_t *const rec = reinterpret_cast<uint32_t *>(recs);
+    if (keep) {
+        for (uint32_t m = hs | hl; m; m &= m - 1) {
+            const uint32_t j = __builtin_ctz(m);
+            if (slot < cand.cap)
+                rec[slot] = (my_pos + j) | (kTruncUnknown << kRecTShift) | (((hs >> j) & 1u) << 31) |
+                            (((hl >> j) & 1u) << 30);
+            ++slot;
+        }
+    }
+    wave_sync_lds();
+    // (slots at or past the count hold stale records: the resolve never reads them)
+    if (lane < cand.cap / 4)
+        *reinterpret_cast<uint4 *>(cand.pos + g * cand.cap + 4 * lane) = recs[lane];
+    if (lane == 0) cand.count[g] = ovf ? cand.cap + 1 : total;
+    wave_sync_lds();
+}
+
+__device__ __forceinline__ void locate_c(const StreamTable &st, uint64_t g, uint32_t &si, uint64_t &off) {
+    uint32_t lo = 0, hi = st.n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cld(st.span_base + mid) <= g) lo = mid; else hi = mid;
+    }
+    si = lo;
+    off = (g - cld(st.span_base + lo)) << st.span_log2;
+}
+
+template <bool kAlign>
+__global__ __launch_bounds__(kDmaW * 64, 1) void scan_dma_kernel(const StreamTable st, const FastParams fp,
+                                                                 const uint64_t *__restrict__ gear,
+                                                                 const Candidates cand, const Compact cp) {
+    __shared__ ScanDmaLds L;
+    const uint64_t *tab = L.tab;
+    for (int i = threadIdx.x; i < 256 * kCopies; i += kDmaW * 64)
+        L.tab[i] = gear[i / kCopies] << fp.tshift;  // pre-shifted GEAR (see FastParams)
+    if (blockIdx.x == 0 && threadIdx.x < kStatWords) cp.stats[threadIdx.x] = 0;  // the resolve accumulates
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t rep = (lane & 31) * 8;
+    const uint64_t span = 1ull << st.span_log2;
+    const uint32_t sub_log2 = st.span_log2 - 6;
+    const uint32_t sub = 1u << sub_log2;   // bytes per lane per span (>= 1 KiB)
+    const uint32_t steps = sub / kStep;    // >= 16
+    const uint32_t lo = lane << sub_log2;
+    const EntryList E{L.epos[wave], L.ehlo[wave], L.ehhi[wave], L.ecnt[wave]};
+    uint4 *const edat = L.edat[wave];
+    const uint64_t src_lane = (uint64_t)(lane & 15) * sub + (lane >> 4) * 16;
+    const uint64_t istride = 16ull * sub;
+    const uint32_t ring0 = (uint32_t)(uintptr_t)&L.ring[wave][0][0];
+    const uint4 *rd0 = &L.ring[wave][0][(lane >> 4) * 64 + (lane & 15)];
+    const uint64_t gstride = (uint64_t)gridDim.x * kDmaW;
+    auto next_full = [&](uint64_t g, uint32_t &si, uint64_t &off) {
+        for (; g < st.total_spans; g += gstride) {
+            locate_c(st, g, si, off);
+            if (cld(st.lens + si) - off >= span) break;
+        }
+        return g;
+    };
+    auto stream_ptr = [&](uint32_t si) {
+        return reinterpret_cast<const uint8_t *>(cld(reinterpret_cast<const uint64_t *>(st.ptrs) + si));
+    };
+    auto issue = [&](const uint8_t *src, uint32_t slot) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds16(src + i * istride, ring0 + slot * 4096 + i * 1024);
+    };
+    // The 48 bytes before a span (its carry-in) by one more DMA; when the span
+    // starts its stream the source is the span itself (in bounds; unused).
+    const uint32_t carry0 = (uint32_t)(uintptr_t)&L.carry[wave][0];
+    auto issue_carry = [&](const uint8_t *b, uint64_t o) {
+        glds4(o != 0 ? b - 48 + 4 * (lane % 12) : b, carry0);
+    };
+    // Two steps in flight while one is hashed: a slot is refilled (step t+2)
+    // as soon as its step has been read into registers.  vmcnt counts the DMAs
+    // and the flush's two stores, in issue order:
+    //   t = 0 (after a flush): step 1 (4) + 2 stores younger  -> vmcnt(6)
+    //   t = 0 (first span):    step 1 (4)                     -> vmcnt(4)
+    //   t = steps-1:           next carry (1) + next step 0 (4) -> vmcnt(5)
+    //   otherwise:             step t+1 (4)                   -> vmcnt(4)
+    uint32_t si;
+    uint64_t off;
+    uint64_t g = next_full((uint64_t)blockIdx.x * kDmaW + wave, si, off);
+    const uint8_t *base = nullptr;
+    if (g < st.total_spans) {
+        base = stream_ptr(si) + off;
+        issue_carry(base, off);
+        issue(base + src_lane, 0);
+        issue(base + src_lane + kStep, 1);
+    }
+    uint32_t slot = 0;  // the slot of the step being hashed (wave-uniform)
+    bool first = true;
+    while (g < st.total_spans) {
+        const uint64_t g_cur = g, off_cur = off;
+        const uint8_t *const base_cur = base;
+        g = next_full(g + gstride, si, off);
+        // The next span's carry bytes and first two steps are issued during
+        // this span's last two steps (when there is none, harmless re-reads
+        // keep the vmcnt counts static).
+        const bool more = g < st.total_spans;
+        const uint8_t *const base_next = more ? stream_ptr(si) + off : base_cur;
+        const uint64_t off_next = more ? off : 0;
+        uint32_t ne = 0;  // quarter entries appended this span (wave-uniform)
+        uint64_t h = 0;
+        uint32_t wb = 0;
+        uint4 F0, F1, F2;
+        for (uint32_t t = 0; t < steps; ++t) {
+            if (t == 0) {
+                if (first) wait_vm<4>(); else wait_vm<6>();
+            } else if (t + 1 == steps) {
+                wait_vm<5>();
+            } else {
+                wait_vm<4>();
+            }
+            Q4 C;
+            const uint4 *rd = rd0 + slot * 256;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) C.q[k] = rd[k * 16];
+            if (t == 0 && lane < 48) wb = L.carry[wave][lane >> 2];  // this span's carry bytes
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // the slot (and carry area) is read
+            if (t + 2 < steps) {
+                issue(base_cur + src_lane + (t + 2) * kStep, slot);
+            } else if (t + 2 == steps) {
+                issue_carry(base_next, off_next);
+                issue(base_next + src_lane, slot);
+            } else {
+                issue(base_next + src_lane + kStep, slot);
+            }
+            if (t == 0) {
+                F0 = C.q[0];
+                F1 = C.q[1];
+                F2 = C.q[2];
+            }
+            process_step_d<kAlign>(C, h, lo + t * kStep, ne, E, edat, tab, rep, fp);
+            slot ^= 1;
+        }
+        first = false;
+        base = base_next;
+        // Fix-up: re-test the first 48 positions with the true carry-in (the
+        // gear hash of the 48 bytes before the span: sum of G[b_i] << (47-i)).
+        wb = (wb >> (8 * (lane & 3))) & 0xFFu;
+        const uint64_t gw = lane < 48 ? L.tab[wb * kCopies + (lane & 31)] << (47 - lane) : 0;
+        const uint64_t hw = wave_total_dpp(gw);
+        h = wave_shr1(h, off_cur != 0 ? hw : 0);
+        {
+            uint64_t h0 = h;
+            append_hits_d(quarter<kAlign>(h, F0, tab, rep, fp) == 0, lo | kEntFix, h0, F0, ne, E, edat);
+            h0 = h;
+            append_hits_d(quarter<kAlign>(h, F1, tab, rep, fp) == 0, (lo + 16) | kEntFix, h0, F1, ne, E, edat);
+            h0 = h;
+            append_hits_d(quarter<kAlign>(h, F2, tab, rep, fp) == 0, (lo + 32) | kEntFix, h0, F2, ne, E, edat);
+        }
+        flush_span_d(g_cur, sub - 1, ne, E, edat, L.recs[wave], tab, rep, fp, cand, lane);
+    }
+    wait_vm<0>();  // no DMA may land after the block's LDS is released
 }
 
 // Ragged last spans of streams (length not a multiple of the span): one wave
@@ -1635,9 +1964,18 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
     // 16 waves per CU (the 128-VGPR budget), GEAR lookups one dword ahead of
     // the chain.  (Measured: 12 waves with two dwords of lookahead is slower.)
     constexpr int W = CDC_SCAN_WAVES, K = CDC_SCAN_LOOK;
+    const uint32_t mode = (fp.diag >> 8) & 3;
+    if (mode == 0 && (fp.diag & kDiagDmaScan)) {  // LDS-DMA input landing (measured, not adopted)
+        const uint64_t groups = (st.total_spans + kDmaW - 1) / kDmaW;
+        const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
+        if (fp.cm_align)
+            scan_dma_kernel<true><<<grid, kDmaW * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+        else
+            scan_dma_kernel<false><<<grid, kDmaW * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+        return hipGetLastError();
+    }
     const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
-    const uint32_t mode = (fp.diag >> 8) & 3;
     if (mode == 1 && fp.cm_align)
         scan_kernel<true, W, K, 1><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else if (mode == 2 && fp.cm_align)

@@ -297,3 +297,17 @@ def test_config4_batch_1024_streams_of_64mib():
         assert_same(got[first[i]:first[i + 1]], oracle.fastcdc(host, *sizes), f"config4 stream {i}")
     del buf, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (512, 2048, 16384), (16384, 65536, 262144)])
+def test_dma_scan_variant_bit_exact(sizes, monkeypatch):
+    """The LDS-DMA scan (A/B path, CHUNKFS_AMD_DIAG bit 10, read at cdc_create):
+    ragged multi-stream batch incl. low-entropy data and a multi-span stream."""
+    import chunkfs_amd as c
+    monkeypatch.setenv("CHUNKFS_AMD_DIAG", "1024")
+    ch = c.FastChunker(c.SizeParams(*sizes))
+    streams = [oracle.splitmix64_bytes(n, 97 + n) for n in (5 * (1 << 20) + 3, 1 << 16, 777, 2 * (1 << 20))]
+    streams.append(np.zeros(3 * (1 << 20) + 11, dtype=np.uint8))
+    streams.append(np.tile(oracle.splitmix64_bytes(61, 5), 40000)[: 2 * (1 << 20) + 5])
+    for data in streams:
+        assert_same(ch.chunk_array(data), oracle.fastcdc(data, *sizes), f"dma {sizes} n={len(data)}")
