@@ -299,6 +299,7 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     HIP_TRY(hipSetDevice(device_));
     hipStream_t s = stream ? stream : own_stream_;
     const double hash_ms = timing_.hash_ms;  // (reported with the batch it hashed)
+    timing_pending_ = false;                 // (a new batch re-records the events)
     timing_ = cdc_timing_t{};
     timing_.hash_ms = hash_ms;
     uint64_t bytes = 0, need = 0;
@@ -416,7 +417,13 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
         const auto t_spin = std::chrono::steady_clock::now();
         while (*done == ~0ull && std::chrono::steady_clock::now() - t_spin < budget) __builtin_ia32_pause();
     }
-    HIP_TRY(hipStreamSynchronize(s));
+    // Once the done word is set every block has written its output (each
+    // fences before taking its ticket; the last one fences system-wide before
+    // the word): the results are complete and the call returns without
+    // waiting for the kernel to retire.  Work the caller queues on this
+    // stream stays ordered after it; the events are read on request (timing()).
+    const bool seen = h_misc[p3::kStatDone] != ~0ull;
+    if (!seen) HIP_TRY(hipStreamSynchronize(s));
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
         set_error(h_misc[p3::kStatDone] != 1 ? "resolve kernel did not report back"
                                              : "chain overflow, output bound or look-back timeout (internal error)");
@@ -435,19 +442,30 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     for (size_t i = n; i-- > 0;)
         if (lens[i] == 0) hf[i] = hf[i + 1];
     std::memcpy(first, hf, (n + 1) * 8);
-    float t01 = 0, t12 = 0, t02 = 0;
-    HIP_TRY(hipEventElapsedTime(&t01, ev_[0], ev_[1]));
-    HIP_TRY(hipEventElapsedTime(&t12, ev_[1], ev_[2]));
-    HIP_TRY(hipEventElapsedTime(&t02, ev_[0], ev_[2]));
-    timing_.scan_ms = t01;
-    timing_.resolve_ms = t12;
+    timing_pending_ = true;
+    if (!seen) (void)timing();
     timing_.compact_ms = 0;  // fused into the resolve kernel
-    timing_.total_ms = t02;
     timing_.candidates = h_misc[p3::kStatCand];
     timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
     timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk];
     timing_.walk_fallback_steps = h_misc[p3::kStatOnDemand];
     return CDC_OK;
+}
+
+const cdc_timing_t &Engine::timing() {
+    if (timing_pending_) {
+        timing_pending_ = false;
+        float t01 = 0, t12 = 0, t02 = 0;
+        if (hipSetDevice(device_) == hipSuccess && hipEventSynchronize(ev_[2]) == hipSuccess &&
+            hipEventElapsedTime(&t01, ev_[0], ev_[1]) == hipSuccess &&
+            hipEventElapsedTime(&t12, ev_[1], ev_[2]) == hipSuccess &&
+            hipEventElapsedTime(&t02, ev_[0], ev_[2]) == hipSuccess) {
+            timing_.scan_ms = t01;
+            timing_.resolve_ms = t12;
+            timing_.total_ms = t02;
+        }
+    }
+    return timing_;
 }
 
 int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
@@ -504,6 +522,7 @@ int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, si
     }
     HIP_TRY(hipSetDevice(device_));
     hipStream_t st = s ? s : own_stream_;
+    (void)timing();  // the last batch's events, before ev_[2] is re-recorded
     HIP_TRY(hipEventRecord(ev_[3], st));
     HIP_TRY(launch_sha256(d_data, d_chunks, n, d_digests, d_counter_, num_cus_, st));
     HIP_TRY(hipEventRecord(ev_[2], st));

@@ -59,7 +59,10 @@ class Engine {
     size_t batch_max_chunks(size_t n, const uint64_t *lens) const;
     int set_gear(const uint64_t *gear);
     const char *describe() const { return describe_.c_str(); }
-    const cdc_timing_t &timing() const { return timing_; }
+    // Kernel durations of the last batch: a FastCDC batch whose done word was
+    // seen returns before its kernels retire, and its events are read here,
+    // on first request.
+    const cdc_timing_t &timing();
     cdc_algo_t algo() const { return algo_; }
     int device() const { return device_; }
     int fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s);
@@ -167,6 +170,7 @@ class Engine {
     unsigned long long *d_counter_ = nullptr;  // SHA-256 work counter
 
     cdc_timing_t timing_{};
+    bool timing_pending_ = false;  // FastCDC events not read yet (see timing())
 
     // Last uploaded stream tables (ptrs ++ lens) and the workspace generation
     // they were uploaded into.

@@ -979,7 +979,16 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 // <= 47 "truncated" positions s+a0 .. s+a0+46, which are tested exactly from
 // the bytes; every later position comes from the scan's records.
 
-constexpr int kResWaves = 4;
+#ifndef CDC_RES_WAVES
+#define CDC_RES_WAVES 8  // 64 spans per block: one block per CU, all resident (r03q/r03r: 4 -> 8 waves, -7 us)
+#endif
+#ifndef CDC_WALK_SPANS
+#define CDC_WALK_SPANS 8
+#endif
+#ifndef CDC_WIN_RECS
+#define CDC_WIN_RECS 768
+#endif
+constexpr int kResWaves = CDC_RES_WAVES;
 constexpr int kResThreads = kResWaves * 64;
 
 // First hitting offset d in [0, tl-a0) of the truncated positions of the
@@ -1176,11 +1185,14 @@ __device__ __forceinline__ void walk_lanes(const StreamTable &st, const FastPara
 //      predecessor's exit).  A failed check waits for the block at fault to
 //      publish its final state; a block whose own entry is stale re-walks;
 //   7. Chunk{offset,length} at the final index, first[] and the statistics.
-constexpr int kWalkSpans = 8;
-constexpr int kWarmSpans = 2;
+constexpr int kWalkSpans = CDC_WALK_SPANS;
+#ifndef CDC_WARM_SPANS
+#define CDC_WARM_SPANS 2
+#endif
+constexpr int kWarmSpans = CDC_WARM_SPANS;
 constexpr int kWinSlots = kWarmSpans + kWalkSpans + 1;  // + 1: searched, never walked
 constexpr int kReach = kWarmSpans + kWalkSpans;         // slots whose records get links
-constexpr uint32_t kWinRecs = 768;  // per-wave record budget (denser windows: global path)
+constexpr uint32_t kWinRecs = CDC_WIN_RECS;  // per-wave record budget (denser windows: global path)
 constexpr uint32_t kVirt = 128;     // virtual entries per wave
 constexpr int kBlockSpans = kResWaves * kWalkSpans;
 constexpr uint64_t kNoDep = ~0ull;  // block entry of a block that starts a stream
