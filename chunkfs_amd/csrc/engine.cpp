@@ -359,11 +359,16 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     }
     rc = is_walk() ? ensure_walk_workspace(spans, n) : ensure_workspace(spans, n);
     if (rc) return rc;
-    // The three per-stream tables are re-uploaded only when they change
-    // (repeated batches over the same device buffers skip the H2D copies).
-    const bool same = ws_gen_ == tables_gen_ && tables_.size() == 2 * n &&
-                      std::memcmp(tables_.data(), h_ptrs, n * 8) == 0 &&
-                      std::memcmp(tables_.data() + n, h_lens, n * 8) == 0;
+    // Small batches (the host path's per-segment calls) read the tables from
+    // the pinned staging block itself: the kernels' few table loads cross
+    // PCIe, but no copy sits on the call's critical path.  Larger batches
+    // re-upload the three per-stream tables only when they change (repeated
+    // batches over the same device buffers skip the H2D copies).
+    const bool zero_copy = bytes <= kSmallBatch && n <= kZeroCopyStreams;
+    const bool same = zero_copy || (ws_gen_ == tables_gen_ && tables_.size() == 2 * n &&
+                                    std::memcmp(tables_.data(), h_ptrs, n * 8) == 0 &&
+                                    std::memcmp(tables_.data() + n, h_lens, n * 8) == 0);
+    cur_tails_ = zero_copy ? h_tails : d_tails_;
     if (!same) {
         HIP_TRY(hipMemcpyAsync(d_ptrs_, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_lens_, h_lens, n * 8, hipMemcpyHostToDevice, s));
@@ -374,9 +379,9 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
         tables_gen_ = ws_gen_;
     }
     StreamTable st{};
-    st.ptrs = d_ptrs_;
-    st.lens = d_lens_;
-    st.span_base = d_span_base_;
+    st.ptrs = zero_copy ? reinterpret_cast<const uint8_t *const *>(h_ptrs) : d_ptrs_;
+    st.lens = zero_copy ? h_lens : d_lens_;
+    st.span_base = zero_copy ? h_sb : d_span_base_;
     st.n = (uint32_t)n;
     st.span_log2 = sl2;
     st.total_spans = spans;
@@ -400,7 +405,7 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     p3::Resolve rs = rs3_;
     rs.gen = ++res_gen_;
     HIP_TRY(hipEventRecord(ev_[0], s));
-    HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, d_tails_, n_tails_, num_cus_, s));
+    HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, cur_tails_, n_tails_, num_cus_, s));
     HIP_TRY(hipEventRecord(ev_[1], s));
     HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, ch3_, cp, rs, d_out, out_cap_, s));
     HIP_TRY(hipEventRecord(ev_[2], s));
@@ -720,6 +725,11 @@ int Engine::init_walk(const uint32_t *seq) {
     if (const char *b = std::getenv("CHUNKFS_AMD_WALK_BYTES"))
         if (std::atoi(b) != 0) wp.nbm = 0;
     if (!wp.nbm) wp.links = 0;  // links are computed over the bitmaps
+    // Wave-cooperative walks (walk.hip wwalk_kernel): Rabin and UltraCDC in
+    // bitmap mode; they replace link mode.  CHUNKFS_AMD_WAVE=0 disables.
+    wp.wave = wp.nbm && (algo_ == CDC_ALGO_RABIN || algo_ == CDC_ALGO_ULTRA) ? 1u : 0u;
+    if (const char *v = std::getenv("CHUNKFS_AMD_WAVE")) wp.wave = wp.wave && std::atoi(v) != 0;
+    if (wp.wave) wp.links = 0;
     wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);
     wp.bm = nullptr;
     // Tables: Rabin mod/out (appending a byte; sliding one out of the window),

@@ -7,7 +7,12 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/chunkfs_amd.h"
@@ -16,6 +21,32 @@
 #include "walk.hpp"
 
 namespace cdc {
+
+// Pageable -> pinned copies of the host path split over a few threads (one
+// core copies ~20 GB/s, below what the H2D DMA takes).  Helpers spin briefly
+// after a job (the next 1 MiB segment usually follows within microseconds),
+// then sleep.  copy() returns when every part is done (hostpath.cpp).
+class CopyPool {
+  public:
+    explicit CopyPool(unsigned threads);
+    ~CopyPool();
+    void copy(void *dst, const void *src, size_t n);
+    unsigned threads() const { return (unsigned)th_.size() + 1; }
+
+  private:
+    void run(unsigned id);
+    void part(unsigned id, unsigned parts);
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<unsigned> left_{0};
+    std::atomic<bool> stop_{false};
+    uint8_t *dst_ = nullptr;
+    const uint8_t *src_ = nullptr;
+    size_t n_ = 0;
+    unsigned parts_ = 1;
+};
 
 class Engine {
   public:
@@ -104,6 +135,10 @@ class Engine {
     uint32_t span_log2_ = 16;
     uint32_t small_span_log2_ = 16;                       // spans of batches <= kSmallBatch bytes
     static constexpr uint64_t kSmallBatch = uint64_t(8) << 20;
+    // Batches this small with few streams read their stream tables straight
+    // from the pinned staging block (no H2D copies: each small copy costs a
+    // ~10 us DMA on the call's critical path).
+    static constexpr size_t kZeroCopyStreams = 64;
     uint32_t cap_ = 0, smax_ = 0;
     std::string describe_;
 
@@ -122,6 +157,7 @@ class Engine {
     p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
     uint64_t res_gen_ = 0;
     uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids
+    const uint64_t *cur_tails_ = nullptr;  // this batch's: d_tails_ or the staging block's
     uint32_t n_tails_ = 0;
     uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
     const uint8_t **d_ptrs_ = nullptr;
@@ -141,7 +177,9 @@ class Engine {
     static constexpr size_t kRingSlot = size_t(4) << 20;
     static constexpr size_t kWriteWindow = size_t(256) << 20;
     static constexpr size_t kRingDirect = size_t(16) << 20;  // chunk_data above this: pageable hipMemcpyAsync
+    static constexpr size_t kUploadPiece = size_t(512) << 10;  // chunk_data: copy of piece k+1 overlaps DMA k
     void *h_ring_ = nullptr;
+    std::unique_ptr<CopyPool> pool_;
     hipEvent_t ring_ev_[kRingSlots] = {};
     uint32_t ring_next_ = 0;
     hipStream_t copy_stream_ = nullptr;

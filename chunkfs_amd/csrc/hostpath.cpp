@@ -23,6 +23,7 @@
 // tests/test_gpu_hostpath.py).
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 #include "engine.hpp"
@@ -45,8 +46,82 @@ double now_s() {
 }
 }  // namespace
 
+// ---- copy pool ----------------------------------------------------------------
+
+CopyPool::CopyPool(unsigned threads) {
+    for (unsigned i = 1; i < threads; ++i) th_.emplace_back([this, i] { run(i); });
+}
+
+CopyPool::~CopyPool() {
+    {
+        std::lock_guard<std::mutex> g(m_);
+        stop_.store(true);
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+}
+
+void CopyPool::part(unsigned id, unsigned parts) {
+    // 4 KiB-aligned part boundaries (whole pages per thread).
+    const size_t step = ((n_ + parts - 1) / parts + 4095) & ~size_t(4095);
+    const size_t a = std::min(n_, step * id), b = std::min(n_, a + step);
+    if (b > a) std::memcpy(dst_ + a, src_ + a, b - a);
+}
+
+void CopyPool::run(unsigned id) {
+    uint64_t seen = 0;
+    for (;;) {
+        // spin ~1 ms for the next job (a streaming write hands over a segment
+        // every ~50 us; a sleeping helper takes ~100 us to wake), then sleep
+        const auto t0 = std::chrono::steady_clock::now();
+        uint64_t g = gen_.load(std::memory_order_acquire);
+        while (g == seen && !stop_.load(std::memory_order_relaxed) &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(1000)) {
+            __builtin_ia32_pause();
+            g = gen_.load(std::memory_order_acquire);
+        }
+        if (g == seen) {
+            std::unique_lock<std::mutex> lk(m_);
+            cv_.wait(lk, [&] { return stop_.load() || gen_.load(std::memory_order_acquire) != seen; });
+            g = gen_.load(std::memory_order_acquire);
+        }
+        if (stop_.load()) return;
+        seen = g;
+        if (id < parts_) part(id, parts_);
+        left_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+}
+
+void CopyPool::copy(void *dst, const void *src, size_t n) {
+    const unsigned helpers = (unsigned)th_.size();
+    if (n < (size_t(1) << 20) || helpers == 0) {  // not worth a hand-off
+        std::memcpy(dst, src, n);
+        return;
+    }
+    dst_ = static_cast<uint8_t *>(dst);
+    src_ = static_cast<const uint8_t *>(src);
+    n_ = n;
+    parts_ = (unsigned)std::min<size_t>(helpers + 1, (n + (size_t(64) << 10) - 1) >> 16);
+    left_.store(helpers, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(m_);  // (pairs with the sleepers' predicate check)
+        gen_.fetch_add(1, std::memory_order_acq_rel);
+    }
+    cv_.notify_all();
+    part(0, parts_);
+    while (left_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+}
+
+// ---- host boundary --------------------------------------------------------------
+
 int Engine::ensure_ring() {
     if (h_ring_) return CDC_OK;
+    if (!pool_) {
+        // CHUNKFS_AMD_COPY_THREADS: threads of the pageable -> pinned copy (default 4)
+        const char *e = std::getenv("CHUNKFS_AMD_COPY_THREADS");
+        const int t = e ? std::atoi(e) : 4;
+        pool_ = std::make_unique<CopyPool>((unsigned)std::max(1, std::min(t, 16)));
+    }
     HIP_TRY(hipHostMalloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocDefault));
     for (auto &e : ring_ev_) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
@@ -87,7 +162,7 @@ int Engine::upload(const uint8_t *src, size_t len, uint8_t *dst, hipStream_t s, 
         ring_next_ = (ring_next_ + 1) % kRingSlots;
         HIP_TRY(hipEventSynchronize(ring_ev_[k]));  // (an event never recorded is complete)
         uint8_t *slot = static_cast<uint8_t *>(h_ring_) + (size_t)k * kRingSlot;
-        std::memcpy(slot, src + off, n);
+        pool_->copy(slot, src + off, n);
         HIP_TRY(hipMemcpyAsync(dst + off, slot, n, hipMemcpyHostToDevice, s));
         HIP_TRY(hipEventRecord(ring_ev_[k], s));
         off += n;
@@ -118,7 +193,10 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
     // stages with several threads (measured 51 vs 31 GiB/s for the single-
     // thread ring on 1 GiB).
     if (len <= kRingDirect) {
-        rc = upload(data, len, d_data_, own_stream_, 256u << 10);
+        // (up to 2 MiB: 512 KiB pieces copied by this thread, so that the copy
+        // of one overlaps the DMA of the previous; larger: 4 MiB pieces copied
+        // by the pool)
+        rc = upload(data, len, d_data_, own_stream_, len <= (size_t(2) << 20) ? kUploadPiece : kRingSlot);
         if (rc) return rc;
     } else {
         HIP_TRY(hipMemcpyAsync(d_data_, data, len, hipMemcpyHostToDevice, own_stream_));

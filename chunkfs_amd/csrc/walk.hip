@@ -680,23 +680,297 @@ __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st
                                                             const WalkState ws) {
     __shared__ uint64_t tab[768];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWalkBlock * kSlot];
-    __shared__ uint64_t nbuf[kNew];
+    __shared__ uint64_t nbuf[kWalkBlock * kNew];
     load_tabs(tab, wp.tabs);
     const Tabs T{tab, tab + 256, tab + 512};
-    if (threadIdx.x != 0) return;
-    for (uint64_t g = ws.flags[2]; g < st.total_spans; ++g) {
-        uint32_t si;
-        uint64_t off;
-        locate(st, g, si, off);
-        if (off == 0) continue;
+    // Lane per stream: streams are independent (every stream's first segment
+    // starts at 0), so each lane runs its own stream's segments in order,
+    // from the lowest segment the last round changed.
+    const uint64_t si = (uint64_t)blockIdx.x * kWalkBlock + threadIdx.x;
+    if (si >= st.n) return;
+    const uint64_t g0 = st.span_base[si], g1 = st.span_base[si + 1];
+    const uint64_t len = st.lens[si];
+    Reader r;
+    bool ready = false;
+    for (uint64_t g = max(g0 + 1, ws.flags[2]); g < g1; ++g) {
         const uint64_t x = ws.X[g - 1];
         if (ws.E[g] == x) continue;
-        const uint64_t len = st.lens[si];
+        const uint64_t off = (g - g0) << st.span_log2;
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
-        Reader r;
-        init_reader<kBits>(r, st, wp, si, len, win + threadIdx.x * kSlot);
-        Hop hp{st.span_base[si], st.span_log2, kNoCand};
-        (void)rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf, hp);
+        if (!ready) {
+            init_reader<kBits>(r, st, wp, (uint32_t)si, len, win + threadIdx.x * kSlot);
+            ready = true;
+        }
+        Hop hp{g0, st.span_log2, kNoCand};
+        (void)rewalk<kAlgo, kBits>(x, g, seg_end, len, r, wp, T, ws, nbuf + threadIdx.x * kNew, hp);
+    }
+}
+
+// ---- wave-cooperative walks (Rabin, UltraCDC; bitmap mode) ------------------
+// One wave per segment, its 64 lanes on ONE chain: a step reads 64 position-
+// words of the bitmaps (4096 positions, coalesced, straight from L2 / HBM)
+// and finds the first event with ballots and a lane scan, so a chain moves
+// thousands of positions per step and the lanes never diverge.  (The lane-
+// per-segment walks above advance 64 positions per lane step, and 64 lanes at
+// unrelated points of their chains pay for each other's cut bookkeeping.)
+// Every chain value (start, cut) is wave-uniform.
+
+// One stream's bitmaps: position-word k of bitmap b at w[k * nbm + b];
+// words at or past nk (the stream end) read 0.
+struct WBm {
+    const uint64_t *w;
+    uint64_t nk;
+    __device__ __forceinline__ uint64_t word(uint32_t nbm, uint32_t b, uint64_t k) const {
+        return k < nk ? w[k * nbm + b] : 0ull;
+    }
+    // 64 bits from position p (bit j = position p + j); p & 63 wave-uniform.
+    __device__ __forceinline__ uint64_t bits64(uint32_t nbm, uint32_t b, uint64_t p) const {
+        const uint64_t k = p >> 6;
+        const uint32_t sh = (uint32_t)(p & 63);
+        const uint64_t lo = word(nbm, b, k);
+        return sh ? (lo >> sh) | (word(nbm, b, k + 1) << (64 - sh)) : lo;
+    }
+};
+
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Bits 0, 8, ..., 56 of x (others zero) gathered into bits 0..7.
+__device__ __forceinline__ uint32_t gather8(uint64_t x) {
+    return (uint32_t)((x * 0x0102040810204080ull) >> 56);
+}
+
+// Per 8-bit block of m: any bit set -> bit t of the result.
+__device__ __forceinline__ uint32_t byte_any(uint64_t m) {
+    m |= m >> 4;
+    m |= m >> 2;
+    m |= m >> 1;
+    return gather8(m & 0x0101010101010101ull);
+}
+
+// Rabin: first hit in [s+min-1, s+end-1], 64 words per step.
+__device__ uint64_t wcut_rabin(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
+    if (n <= wp.min) return n;
+    const uint64_t end = n < wp.max ? n : wp.max;
+    const uint64_t lo = s + wp.min - 1, hi = s + end - 1;
+    const uint64_t klo = lo >> 6, khi = hi >> 6;
+    for (uint64_t k0 = klo; k0 <= khi; k0 += 64) {
+        const uint64_t k = k0 + lane;
+        uint64_t w = k <= khi ? B.word(1, 0, k) : 0ull;
+        if (k == klo) w &= ~0ull << (lo & 63);
+        if (k == khi && (hi & 63) != 63) w &= (2ull << (hi & 63)) - 1;
+        const uint64_t m = __ballot(w != 0);
+        if (m) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(m);
+            return (k0 + f) * 64 + (uint64_t)__builtin_ctzll(rdlane64(w, f)) - s + 1;
+        }
+    }
+    return end;
+}
+
+// UltraCDC over bitmaps 0 (mask_s hit), 1 (mask_l hit), 2 (8-byte repeat),
+// 512 blocks per step, lane l on blocks 8l .. 8l+7 of the step.  Per block
+// (cut_ultra): a repeat counts towards LEST (cut at its end when the run of
+// repeats reaches LEST), otherwise the run resets and the block's first hit
+// (mask by the block's side of the normal size) cuts.  The run entering each
+// lane is a scan of per-lane maps x -> (all 8 repeat ? x + 8 : trailing
+// repeats), the run carried in from the previous step included.
+__device__ uint64_t wcut_ultra(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
+    if (n <= wp.min) return n;
+    uint64_t normal = wp.avg, end = n;
+    if (n >= wp.max) end = wp.max;
+    else if (n <= normal) normal = n;
+    if (end < (uint64_t)wp.min + 8) return end;
+    const uint64_t nblk = (end - wp.min) >> 3;                                    // blocks with i + 8 <= end
+    const uint64_t tnorm = normal > wp.min ? (normal - wp.min + 7) >> 3 : 0;  // first block at / after normal
+    uint32_t lec = 0;
+    for (uint64_t t0 = 0; t0 < nblk; t0 += 512) {
+        const uint64_t tl = t0 + 8ull * lane;
+        const uint64_t P = s + wp.min + 8 * tl;
+        const uint64_t hs = B.bits64(3, 0, P), hl = B.bits64(3, 1, P), eq = B.bits64(3, 2, P);
+        const uint32_t nv = tl < nblk ? (uint32_t)min(nblk - tl, (uint64_t)8) : 0u;
+        const uint32_t vb = (1u << nv) - 1;
+        const uint64_t split = tnorm > tl ? min(tnorm - tl, (uint64_t)8) : 0ull;
+        const uint64_t lowm = split >= 8 ? ~0ull : (1ull << (8 * split)) - 1;
+        const uint64_t m = (hs & lowm) | (hl & ~lowm);
+        const uint32_t r = gather8(eq & 0x0101010101010101ull) & vb;
+        const uint32_t a_hit = ~r & byte_any(m) & vb;
+        const uint32_t lead = (uint32_t)__builtin_ctz(~r);                     // leading repeats (<= 8)
+        const uint32_t z = ~r & 0xFFu;
+        uint32_t fa = r == 0xFFu, fv = fa ? 8u : (uint32_t)__builtin_clz(z) - 24u;  // trailing repeats
+        // inclusive scan of the maps (composition: later lane after earlier)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t pa = (uint32_t)__shfl_up((int)fa, o), pv = (uint32_t)__shfl_up((int)fv, o);
+            if (lane >= (uint32_t)o) {
+                fv = fa ? pv + fv : fv;
+                fa = fa & pa;
+            }
+        }
+        const uint32_t cout = fa ? lec + fv : fv;
+        const uint32_t up = (uint32_t)__shfl_up((int)cout, 1);
+        const uint32_t cin = lane ? up : lec;
+        const uint32_t tb0 = cin >= CDC_ULTRA_LEST - 1 ? 0u : CDC_ULTRA_LEST - 1 - cin;
+        const uint32_t tB = tb0 < lead ? tb0 : 8u;
+        const uint32_t tA = (uint32_t)__builtin_ctz(a_hit | 0x100u);
+        const uint32_t te = min(tA, tB);
+        const uint64_t ev = __ballot(te < 8);
+        if (ev) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(ev);
+            const uint32_t tf = (uint32_t)__builtin_amdgcn_readlane((int)te, (int)f);
+            const uint32_t isb = (uint32_t)__builtin_amdgcn_readlane((int)(tB < tA), (int)f);
+            const uint64_t i = wp.min + 8 * (t0 + 8ull * f + tf);
+            if (isb) return i + 8;
+            const uint64_t mf = rdlane64(m, f);
+            return i + (uint64_t)__builtin_ctzll((mf >> (8 * tf)) & 0xFFull);
+        }
+        lec = (uint32_t)__builtin_amdgcn_readlane((int)cout, 63);
+    }
+    return end;
+}
+
+template <int kAlgo>
+__device__ __forceinline__ uint64_t wcut(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
+    if constexpr (kAlgo == 2) return wcut_rabin(B, s, n, wp, lane);
+    else return wcut_ultra(B, s, n, wp, lane);
+}
+
+// walk_kernel with a wave per segment (4 segments per 256-thread block).
+template <int kAlgo>
+__global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
+    constexpr uint32_t nbm = kAlgo == 2 ? 1 : 3;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
+    const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6};
+    uint64_t c = 0;
+    if (off != 0) {  // warm-up start as walk_kernel (max-length grid)
+        c = off > wp.warm ? off - wp.warm : 0;
+        c = c / wp.max * wp.max;
+        while (c < off) c += wcut<kAlgo>(B, c, len - c, wp, lane);
+    }
+    if (lane == 0) ws.E[g] = c;
+    uint32_t cnt = 0;
+    uint64_t *list = ws.list + g * wp.cap;
+    while (c < seg_end) {
+        if (lane == 0 && cnt < wp.cap) list[cnt] = c;
+        ++cnt;
+        c += wcut<kAlgo>(B, c, len - c, wp, lane);
+    }
+    if (lane == 0) {
+        ws.X[g] = c;
+        ws.N[g] = cnt;
+        if (cnt > wp.cap) atomicAdd(&ws.flags[1], 1ull);
+    }
+}
+
+// rewalk() for one wave (wave-uniform chain; lane 0 writes): re-walk segment g
+// from x until the new chain meets the old one (<= kNew new starts, kept in
+// the wave's LDS slots), else a full walk.  xo = the segment's exit after it.
+template <int kAlgo>
+__device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, const WBm &B, const WalkParams &wp,
+                        const WalkState &ws, uint64_t *nb, uint32_t lane, uint64_t &xo) {
+    uint64_t *list = ws.list + g * wp.cap;
+    const uint32_t n_old = ws.N[g];
+    const uint32_t lim = min(n_old, wp.cap);
+    const uint64_t x_old = ws.X[g];
+    uint64_t c = x;
+    uint32_t m = 0, j = 0;
+    while (c < seg_end && m < kNew) {
+        while (j < lim && list[j] < c) ++j;
+        if (j < lim && list[j] == c) {  // meets the old chain at old start j
+            if (lane == 0) {
+                if (m < j) {
+                    for (uint32_t k = j; k < lim; ++k) list[m + k - j] = list[k];
+                } else if (m > j) {
+                    for (uint32_t k = lim; k-- > j;)
+                        if (m + k - j < wp.cap) list[m + k - j] = list[k];
+                }
+                for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
+                ws.E[g] = x;
+                ws.N[g] = m + (n_old - j);
+                if (m + (n_old - j) > wp.cap) atomicAdd(&ws.flags[1], 1ull);
+            }
+            xo = x_old;
+            return false;
+        }
+        if (lane == 0) nb[m] = c;
+        ++m;
+        c += wcut<kAlgo>(B, c, len - c, wp, lane);
+    }
+    if (c >= seg_end) {  // the whole segment in <= kNew starts, no meeting point
+        if (lane == 0) {
+            for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
+            ws.E[g] = x;
+            ws.N[g] = m;
+            ws.X[g] = c;
+        }
+        xo = c;
+        return c != x_old;
+    }
+    // full walk from x
+    c = x;
+    uint32_t cnt = 0;
+    while (c < seg_end) {
+        if (lane == 0 && cnt < wp.cap) list[cnt] = c;
+        ++cnt;
+        c += wcut<kAlgo>(B, c, len - c, wp, lane);
+    }
+    if (lane == 0) {
+        ws.E[g] = x;
+        ws.X[g] = c;
+        ws.N[g] = cnt;
+        if (cnt > wp.cap) atomicAdd(&ws.flags[1], 1ull);
+    }
+    xo = c;
+    return c != x_old;
+}
+
+// fix_kernel with a wave per segment: same schedule (snapshots Es / Xs, run
+// ahead into unscheduled successors), wave-cooperative re-walks.
+template <int kAlgo>
+__global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
+    if (ws.gate && *ws.gate == 0) return;  // the previous round settled everything
+    constexpr uint32_t nbm = kAlgo == 2 ? 1 : 3;
+    __shared__ uint64_t nbuf[4 * kNew];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    if (off == 0) return;  // a stream's first segment starts exactly at 0
+    uint64_t x = ws.Xs[g - 1];
+    if (ws.Es[g] == x) return;
+    const uint64_t len = st.lens[si];
+    const uint64_t span = 1ull << st.span_log2;
+    const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6};
+    uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
+    uint64_t gg = g;
+    for (uint32_t k = 0;; ++k) {
+        const uint64_t seg_end = min(off + span, len);
+        if (lane == 0) atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
+        uint64_t xo;
+        if (!wrewalk<kAlgo>(x, gg, seg_end, len, B, wp, ws, nb, lane, xo)) break;
+        if (seg_end >= len) break;  // the stream's last segment: no successor
+        if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
+            if (lane == 0) {
+                atomicAdd(&ws.flags[0], 1ull);  // a successor needs another round
+                atomicMin(&ws.flags[2], (unsigned long long)gg);
+            }
+            break;
+        }
+        x = xo;
+        ++gg;
+        off += span;
     }
 }
 
@@ -1116,7 +1390,7 @@ hipError_t walk_dispatch(int which, const StreamTable &st, const WalkParams &wp,
     const unsigned blocks = (unsigned)((st.total_spans + kWalkBlock - 1) / kWalkBlock);
     if (which == 0) walk_kernel<kAlgo, kBits><<<blocks, kWalkBlock, 0, s>>>(st, wp, ws);
     else if (which == 1) fix_kernel<kAlgo, kBits><<<blocks, kWalkBlock, 0, s>>>(st, wp, ws);
-    else serial_kernel<kAlgo, kBits><<<1, kWalkBlock, 0, s>>>(st, wp, ws);
+    else serial_kernel<kAlgo, kBits><<<(st.n + kWalkBlock - 1) / kWalkBlock, kWalkBlock, 0, s>>>(st, wp, ws);
     return hipGetLastError();
 }
 
@@ -1154,6 +1428,12 @@ hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t
 }
 
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
+    if (wp.wave && wp.nbm && st.total_spans && (wp.algo == 2 || wp.algo == 4)) {
+        const unsigned blocks = (unsigned)((st.total_spans + 3) / 4);
+        if (wp.algo == 2) wwalk_kernel<2><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else wwalk_kernel<4><<<blocks, 256, 0, s>>>(st, wp, ws);
+        return hipGetLastError();
+    }
     return dispatch(0, st, wp, ws, s);
 }
 
@@ -1163,6 +1443,12 @@ hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkSta
     if (e != hipSuccess) return e;
     e = hipMemcpyAsync(ws.Es, ws.E, st.total_spans * 8, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;
+    if (wp.wave && wp.nbm && (wp.algo == 2 || wp.algo == 4)) {
+        const unsigned blocks = (unsigned)((st.total_spans + 3) / 4);
+        if (wp.algo == 2) wfix_kernel<2><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else wfix_kernel<4><<<blocks, 256, 0, s>>>(st, wp, ws);
+        return hipGetLastError();
+    }
     return dispatch(1, st, wp, ws, s);
 }
 

@@ -37,6 +37,7 @@ struct WalkParams {
     uint32_t seg_words;       // 64-bit words per segment and bitmap (segment bytes / 64)
     uint32_t bits_fine;       // bitmap pass: lane per 64-position word (Ultra, Leap, Seq)
     uint32_t ahead;           // fix-up round: segments one lane may re-walk (1 = plain Jacobi)
+    uint32_t wave;            // 1: wave-cooperative walk_kernel (Rabin / UltraCDC bitmap mode)
     // Link mode (LeapCDC): the rule's candidate cut positions (content-defined:
     // every cut that is not a max / end cut lands on one) are listed per
     // segment, and the next chunk start after a chunk starting at each of
