@@ -424,6 +424,50 @@ def algo_lines(args, eng, w, steps):
     return res
 
 
+def lowentropy_walk_lines(args, eng, nbytes=256 << 20):
+    """Rabin / UltraCDC / LeapCDC / SeqCDC on low-entropy device streams of
+    `nbytes` (zeros; a 61-byte period), bench sizes: chains from different
+    starts never merge on such data, so these lines time the fix-up rounds
+    and the in-order pass (one wave per stream) that the splitmix64 lines
+    never reach.  Device GiB/s, the re-walk statistics and bit-exactness vs
+    the oracle (parity vs the crate is unpinned)."""
+    import numpy as np
+    import torch
+    import chunkfs_amd as cfa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    n = nbytes
+    period = torch.from_numpy(oracle.splitmix64_bytes(61, 7)).to(eng.dev)
+    inputs = {"zeros": torch.zeros(n, dtype=torch.uint8, device=eng.dev),
+              "periodic61": period.repeat(-(-n // 61))[:n].contiguous()}
+    sizes = cfa.SizeParams(args.min, args.avg, args.max)
+    res = {}
+    for inp, buf in inputs.items():
+        host = buf.cpu().numpy() if not args.no_parity else None
+        for name in ("rabin", "ultra", "leap", "seq"):
+            cls = {"rabin": cfa.RabinChunker, "ultra": cfa.UltraChunker, "leap": cfa.LeapChunker}.get(name)
+            ch = cls(sizes, device=eng.local) if cls else cfa.SeqChunker(0, sizes, device=eng.local)
+            cap = ch.batch_max_chunks([n])
+            out = torch.empty((cap, 2), dtype=torch.int64, device=eng.dev)
+            first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            first = ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            t = ch.last_timing()
+            line = {"GiBps": n / el / (1 << 30), "chunks": int(first[1]),
+                    "rewalked_segments": t["fixup_iterations"], "in_order_pass": bool(t["overflow_spans"])}
+            if host is not None:
+                got = out[:int(first[1])].cpu().numpy().view(np.uint64)
+                ref = oracle.cdc(name, host, args.min, args.avg, args.max)
+                line["parity_vs_oracle"] = bool(got.shape == ref.shape and (got == ref).all())
+            res[f"{name}_{inp}"] = line
+            ch.close()
+            del out
+    return {"bytes": int(n), "sizes": [args.min, args.avg, args.max], "lines": res}
+
+
 def config5_lines(args, eng, w, steps=2):
     """Config 5's size sweep (BASELINE.json configs[4]) on one GPU: UltraCDC and
     LeapCDC (plus Rabin and Seq) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg
@@ -682,6 +726,7 @@ def main(argv=None):
             extras["sweep"] = sweep_lines(args, eng, w, max(5, args.steps // 2))
         if not args.no_algos and args.workload == "stream":
             extras["other_chunkers"] = algo_lines(args, eng, w, 3)
+            extras["other_chunkers_low_entropy"] = lowentropy_walk_lines(args, eng)
             extras["config3"] = config3_line(args, local)
             extras["config5_1gpu"] = config5_lines(args, eng, w)
         if args.cpu_seconds > 0:

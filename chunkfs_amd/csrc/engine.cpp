@@ -668,15 +668,33 @@ int Engine::init_walk(const uint32_t *seq) {
     // fix-up re-walks; profiles/r02ak_walk_avg64k_segments.log), a warm-up of
     // 8 avg (a chain from an arbitrary start merges with the true one within a
     // few content-defined cuts).
-    seg_log2_ = 15;
+    // Bitmap mode (DESIGN.md): Rabin when every tested digest is a full
+    // window (min >= 48), UltraCDC, LeapCDC, and SeqCDC when its run length
+    // fits a 64-bit step (seq_length <= 63).  CHUNKFS_AMD_WALK_BYTES=1 forces
+    // the byte walks (A/B experiments).
+    wp.nbm = algo_ == CDC_ALGO_RABIN ? (min_ >= CDC_RABIN_WINDOW ? 1u : 0u)
+           : algo_ == CDC_ALGO_ULTRA ? 3u : algo_ == CDC_ALGO_LEAP ? 2u
+           : (wp.seq_len <= 63 ? 1u : 0u);
+    if (const char *b = std::getenv("CHUNKFS_AMD_WALK_BYTES"))
+        if (std::atoi(b) != 0) wp.nbm = 0;
+    // Wave-cooperative walks (walk.hip wwalk_kernel, one wave per segment)
+    // for every rule in bitmap mode.  CHUNKFS_AMD_WAVE=0 disables.
+    wp.wave = wp.nbm ? 1u : 0u;
+    if (const char *v = std::getenv("CHUNKFS_AMD_WAVE")) wp.wave = wp.wave && std::atoi(v) != 0;
+    // Lane walks: 32 KiB segments whatever the average (profiles/r02ak).
+    // Wave walks: 128 KiB (Rabin, Leap) / 256 KiB segments, 8 avg warm-up
+    // (profiles/r03_walk/r03w_walk_seg_sweep.txt: a wave walks thousands of
+    // positions per step, so fewer, longer segments cut the warm-up share).
+    seg_log2_ = !wp.wave ? 15 : algo_ == CDC_ALGO_RABIN || algo_ == CDC_ALGO_LEAP ? 17 : 18;
     // The per-segment start list holds segment/min + 2 entries: keep it <= ~4k
     // (tiny min), and segments >= 4 KiB.
     const uint32_t lmin = 63 - (uint32_t)__builtin_clzll((uint64_t)min_) + 12;
     if (seg_log2_ > lmin) seg_log2_ = lmin < 12 ? 12 : lmin;
-    // SeqCDC chains (jumps skip most positions) merge more slowly: 16 avg
-    // (profiles/r02ag_walk_warm_sweep.log: 226 -> 241 GiB/s; the other rules
-    // gain nothing from a longer warm-up).
-    uint64_t warm_mult = algo_ == CDC_ALGO_SEQ ? 16 : 8;
+    // SeqCDC chains (jumps skip most positions) merge more slowly: 16 avg for
+    // the lane walks (profiles/r02ag_walk_warm_sweep.log: 226 -> 241 GiB/s;
+    // the other rules gain nothing from a longer warm-up); 8 avg for all
+    // wave walks.
+    uint64_t warm_mult = algo_ == CDC_ALGO_SEQ && !wp.wave ? 16 : 8;
     if (const char *w = std::getenv("CHUNKFS_AMD_WALK")) {
         unsigned a = 0, b = 0;
         if (std::sscanf(w, "%u,%u", &a, &b) == 2 && a >= 10 && a <= 30) {
@@ -715,21 +733,8 @@ int Engine::init_walk(const uint32_t *seq) {
         while (cc < 4 * expect && cc < 1024) cc <<= 1;
         wp.ccap = (uint32_t)cc;
     }
-    // Bitmap mode (DESIGN.md): Rabin when every tested digest is a full
-    // window (min >= 48), UltraCDC, LeapCDC, and SeqCDC when its run length
-    // fits a 64-bit step (seq_length <= 63).  CHUNKFS_AMD_WALK_BYTES=1 forces
-    // the byte walks (A/B experiments).
-    wp.nbm = algo_ == CDC_ALGO_RABIN ? (min_ >= CDC_RABIN_WINDOW ? 1u : 0u)
-           : algo_ == CDC_ALGO_ULTRA ? 3u : algo_ == CDC_ALGO_LEAP ? 2u
-           : (wp.seq_len <= 63 ? 1u : 0u);
-    if (const char *b = std::getenv("CHUNKFS_AMD_WALK_BYTES"))
-        if (std::atoi(b) != 0) wp.nbm = 0;
     if (!wp.nbm) wp.links = 0;  // links are computed over the bitmaps
-    // Wave-cooperative walks (walk.hip wwalk_kernel): Rabin and UltraCDC in
-    // bitmap mode; they replace link mode.  CHUNKFS_AMD_WAVE=0 disables.
-    wp.wave = wp.nbm && (algo_ == CDC_ALGO_RABIN || algo_ == CDC_ALGO_ULTRA) ? 1u : 0u;
-    if (const char *v = std::getenv("CHUNKFS_AMD_WAVE")) wp.wave = wp.wave && std::atoi(v) != 0;
-    if (wp.wave) wp.links = 0;
+    if (wp.wave) wp.links = 0;  // the wave walks replace link mode
     wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);
     wp.bm = nullptr;
     // Tables: Rabin mod/out (appending a byte; sliding one out of the window),
@@ -766,6 +771,8 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
     const size_t oF = take((N + 1) * 8), oG = take((4 + 4 * walk::kMaxFixRounds) * 8);
     const size_t oBM = take(S * (size_t)wp_.seg_words * wp_.nbm * 8);  // predicate bitmaps
+    const bool jt = algo_ == CDC_ALGO_LEAP && wp_.wave;
+    const size_t oJT = take(jt ? S * (size_t)wp_.seg_words * 24 : 0);  // LeapCDC word tables
     const size_t cc = wp_.links ? wp_.ccap : 0;                          // link mode
     const size_t oCN = take(S * 4), oCP = take(S * cc * 4), oLN = take(S * cc * 8), oLI = take(S * cc * 4);
     const size_t vc = wp_.links ? S * 8 : 0;
@@ -792,6 +799,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wst_.first = reinterpret_cast<uint64_t *>(b + oF);
     wst_.flags = reinterpret_cast<unsigned long long *>(b + oG);
     wp_.bm = wp_.nbm ? reinterpret_cast<uint64_t *>(b + oBM) : nullptr;
+    wp_.jt = jt ? reinterpret_cast<uint8_t *>(b + oJT) : nullptr;
     wp_.ccnt = reinterpret_cast<uint32_t *>(b + oCN);
     wp_.cpos = reinterpret_cast<uint32_t *>(b + oCP);
     wp_.lnext = reinterpret_cast<uint64_t *>(b + oLN);

@@ -720,6 +720,8 @@ __global__ __launch_bounds__(kWalkBlock) void serial_kernel(const StreamTable st
 struct WBm {
     const uint64_t *w;
     uint64_t nk;
+    const uint8_t *jt = nullptr;  // LeapCDC: the stream's word tables
+    uint8_t *lb = nullptr;        // LeapCDC: the wave's LDS slot (64 words x 24 B)
     __device__ __forceinline__ uint64_t word(uint32_t nbm, uint32_t b, uint64_t k) const {
         return k < nk ? w[k * nbm + b] : 0ull;
     }
@@ -832,16 +834,241 @@ __device__ uint64_t wcut_ultra(const WBm &B, uint64_t s, uint64_t n, const WalkP
     return end;
 }
 
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, o), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), o);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// SeqCDC over bitmap 0 (pair p in the mode's direction), a window of 4096
+// positions per load (lane l on positions 64l .. 64l+63 of it).  From a
+// restart point t0 (the chunk's min, or a jump's landing) the rule is two
+// events, whichever comes first: a run of seq_length in-direction pairs
+// completes at t (cut after t), or the jump_trigger-th opposing pair since the
+// restart is at t (jump: the next restart is t + jump_size).  Run ends come
+// from shifted ANDs (the previous lane's word carried in; lane 0: the run
+// carried from the previous window); the n-th opposing pair from a lane
+// prefix of popcounts and a select in the one lane that holds it.  Several
+// restarts per window are handled from the same registers.
+__device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
+    if (n <= wp.min) return n;
+    const uint64_t end = n < wp.max ? n : wp.max;
+    const uint32_t L = wp.seq_len, TT = wp.seq_trig, J = wp.seq_jump;
+    uint64_t i = wp.min;        // window start (relative to s)
+    uint32_t cnt = 0, opp = 0;  // run / opposing pairs carried into the window
+    while (i < end) {
+        const uint64_t lim = end - i;  // valid positions of the window: t < lim
+        const uint64_t tl = 64ull * lane;
+        const uint64_t vm = tl >= lim ? 0ull : (lim - tl >= 64 ? ~0ull : (1ull << (lim - tl)) - 1);
+        const uint64_t y = B.bits64(1, 0, s + i + tl) & vm;
+        const uint64_t z = ~y & vm;
+        uint64_t yp = shfl_up64(y, 1);
+        if (lane == 0) yp = cnt ? ~0ull << (64 - cnt) : 0ull;
+        uint64_t a = y;
+        for (uint32_t q = 1; q < L; ++q) a &= (y << q) | (yp >> (64 - q));
+        const uint32_t zc = (uint32_t)__popcll(z);
+        uint32_t zin = zc;  // inclusive prefix of opposing pairs over lanes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)zin, o);
+            if (lane >= (uint32_t)o) zin += v;
+        }
+        const uint32_t zex = zin - zc;
+        uint64_t t0 = 0;  // restart offset in the window
+        uint32_t opp0 = opp;
+        bool carried = true;  // t0 = 0 with the carried run and count
+        for (;;) {
+            // run event: a run end at t >= thr (all its pairs at >= t0)
+            const uint64_t thr = carried ? 0 : t0 + L - 1;
+            const uint64_t am = thr <= tl ? a : (thr - tl >= 64 ? 0ull : a & (~0ull << (thr - tl)));
+            const uint64_t mr = __ballot(am != 0);
+            uint64_t tr = 4096;
+            if (mr) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(mr);
+                tr = 64ull * f + (uint64_t)__builtin_ctzll(rdlane64(am, f));
+            }
+            // jump event: the (TT - opp0)-th opposing pair at or after t0
+            uint32_t before = 0;
+            if (t0) {
+                const uint32_t l0 = (uint32_t)(t0 >> 6), b0 = (uint32_t)(t0 & 63);
+                const uint64_t zl = rdlane64(z, l0);
+                before = (uint32_t)__builtin_amdgcn_readlane((int)zex, (int)l0) +
+                         (b0 ? (uint32_t)__popcll(zl & ((1ull << b0) - 1)) : 0u);
+            }
+            const uint32_t target = before + (TT - opp0);
+            const uint64_t mj = __ballot(zin >= target);
+            uint64_t tj = 4096;
+            if (mj) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(mj);
+                const uint32_t need = target - (uint32_t)__builtin_amdgcn_readlane((int)zex, (int)f);
+                tj = 64ull * f + select_bit(rdlane64(z, f), need);
+            }
+            if (tr < tj) return i + tr + 1;  // (tr < lim: bits past the end are clear)
+            if (tj >= 4096) {
+                if (lim <= 4096) return end;
+                // no event in [t0, 4096): carry the run ending at 4095 and the count
+                const uint64_t y63 = rdlane64(y, 63);
+                const uint32_t r63 = ~y63 ? (uint32_t)__builtin_clzll(~y63) : 64u;
+                cnt = (uint32_t)min((uint64_t)r63, 4096 - t0);
+                opp = opp0 + ((uint32_t)__builtin_amdgcn_readlane((int)zin, 63) - before);
+                i += 4096;
+                break;
+            }
+            // jump
+            t0 = tj + J;
+            opp0 = 0;
+            carried = false;
+            if (t0 >= 4096 || t0 >= lim) {
+                i += t0;
+                cnt = 0;
+                opp = 0;
+                break;
+            }
+        }
+    }
+    return end;
+}
+
+// ---- LeapCDC: leap rule over two words, word tables, wave walk ---------------
+// Candidate C at offset x (0..63) of word w: its 24 windows end at C-1 ..
+// C-24, all inside words w-1 (lo) and w (hi) of the primary (p*) and
+// secondary (s*) bitmaps.  Returns the leap (1..24), or 0 when C is accepted
+// (cut_leap_bits: the nearest failing primary window at field bit j leaps
+// 3 + j; then the secondary windows C-23, C-24 leap 2, 1).
+static_assert(CDC_LEAP_WINDOWS == CDC_LEAP_PRIMARY + 2, "two secondary windows");
+
+__device__ __forceinline__ uint32_t leap_step(uint64_t plo, uint64_t phi, uint64_t slo, uint64_t shi, uint32_t x) {
+    constexpr uint32_t kP = CDC_LEAP_PRIMARY;
+    const uint32_t t = x + 64 - kP;  // bit of position C - 22 in (hi:lo)
+    const uint64_t f = (t < 64 ? (plo >> t) | (phi << (64 - t)) : phi >> (t - 64)) & ((1ull << kP) - 1);
+    const uint64_t z = ~f & ((1ull << kP) - 1);
+    if (z) return CDC_LEAP_WINDOWS - (kP - 1 - (63u - (uint32_t)__builtin_clzll(z)));
+    const uint32_t t2 = x + 63 - kP;  // C - 23
+    if (!(((t2 < 64 ? slo >> t2 : shi >> (t2 - 64))) & 1)) return CDC_LEAP_WINDOWS - kP;
+    const uint32_t t3 = t2 - 1;       // C - 24
+    if (!(((t3 < 64 ? slo >> t3 : shi >> (t3 - 64))) & 1)) return CDC_LEAP_WINDOWS - kP - 1;
+    return 0;
+}
+
+// Word tables: wave per segment (4 per block), lane per word.
+__global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const WalkParams wp) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint64_t base = st.span_base[si] * (uint64_t)wp.seg_words;
+    const uint64_t *bm = wp.bm + base * 2;
+    uint8_t *jt = wp.jt + base * 24;
+    const uint64_t nk = (len + 63) >> 6;
+    for (uint32_t r = 0; r < wp.seg_words / 64; ++r) {
+        const uint64_t w = (off >> 6) + (uint64_t)r * 64 + lane;
+        if (w >= nk) return;
+        const uint64_t phi = bm[2 * w], shi = bm[2 * w + 1];
+        const uint64_t plo = w ? bm[2 * w - 2] : 0ull, slo = w ? bm[2 * w - 1] : 0ull;
+        // Entry e's orbit usually lands on entry e-1's within a leap or two
+        // (consecutive candidates share their nearest failing window): `vis`
+        // holds the positions of the word whose orbit result is `pv`, and an
+        // orbit that reaches one of them takes that result.
+        uint32_t o[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t vis = 0;
+        uint32_t pv = 0;
+#pragma unroll
+        for (int e = 0; e < 24; ++e) {
+            uint32_t x = (uint32_t)e, v;
+            uint64_t mine = 0;
+            bool merged = false;
+            for (;;) {
+                if ((vis >> x) & 1) { v = pv; merged = true; break; }
+                mine |= 1ull << x;
+                const uint32_t l = leap_step(plo, phi, slo, shi, x);
+                if (!l) { v = 64 + x; break; }
+                x += l;
+                if (x >= 64) { v = x - 64; break; }
+            }
+            vis = merged ? vis | mine : mine;
+            pv = v;
+            o[e >> 2] |= v << (8 * (e & 3));
+        }
+        uint64_t *d = reinterpret_cast<uint64_t *>(jt + w * 24);
+        d[0] = ((uint64_t)o[1] << 32) | o[0];
+        d[1] = ((uint64_t)o[3] << 32) | o[2];
+        d[2] = ((uint64_t)o[5] << 32) | o[4];
+    }
+}
+
+// The leap rule from candidate C (wave-uniform), words read straight from
+// the bitmaps (broadcast loads).
+__device__ __forceinline__ uint32_t leap_at(const WBm &B, uint64_t C) {
+    const uint64_t w = C >> 6;
+    const uint64_t phi = B.word(2, 0, w), shi = B.word(2, 1, w);
+    const uint64_t plo = w ? B.word(2, 0, w - 1) : 0ull, slo = w ? B.word(2, 1, w - 1) : 0ull;
+    return leap_step(plo, phi, slo, shi, (uint32_t)(C & 63));
+}
+
+// cut_leap_bits for one wave: direct leaps to the first word boundary, then
+// word tables 64 words at a time (the wave stages them in its LDS slot, one
+// word per lane, and follows the orbit through them), then direct leaps in
+// the word holding the bound (tables may accept past it).
+__device__ uint64_t wcut_leap(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
+    if (n <= wp.min) return n;
+    const uint64_t end = n < wp.max ? n : wp.max;
+    const uint64_t E = s + end;  // candidates C <= E
+    uint64_t C = s + wp.min;
+    const uint64_t wb = (C >> 6) + 1;
+    while (C < 64 * wb) {
+        if (C > E) return end;
+        const uint32_t l = leap_at(B, C);
+        if (!l) return C - s;
+        C += l;
+    }
+    uint64_t w = C >> 6;
+    uint32_t e = (uint32_t)(C & 63);
+    if (E >= 63) {
+        const uint64_t wl = (E - 63) >> 6;  // last word wholly <= E
+        while (w <= wl) {
+            const uint32_t nw = (uint32_t)min(wl - w + 1, (uint64_t)64);
+            if (lane < nw) {
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(B.jt + (w + lane) * 24);
+                uint64_t *dst = reinterpret_cast<uint64_t *>(B.lb + lane * 24);
+                dst[0] = src[0];
+                dst[1] = src[1];
+                dst[2] = src[2];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t j = 0; j < nw; ++j) {
+                const uint32_t v = B.lb[j * 24 + e];
+                if (v >= 64) return 64 * (w + j) + (v - 64) - s;
+                e = v;
+            }
+            w += nw;
+            __builtin_amdgcn_wave_barrier();  // (the slot is rewritten next round)
+        }
+    }
+    C = 64 * w + e;
+    while (C <= E) {
+        const uint32_t l = leap_at(B, C);
+        if (!l) return C - s;
+        C += l;
+    }
+    return end;
+}
+
 template <int kAlgo>
 __device__ __forceinline__ uint64_t wcut(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
     if constexpr (kAlgo == 2) return wcut_rabin(B, s, n, wp, lane);
+    else if constexpr (kAlgo == 6) return wcut_seq(B, s, n, wp, lane);
+    else if constexpr (kAlgo == 5) return wcut_leap(B, s, n, wp, lane);
     else return wcut_ultra(B, s, n, wp, lane);
 }
 
 // walk_kernel with a wave per segment (4 segments per 256-thread block).
 template <int kAlgo>
 __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
-    constexpr uint32_t nbm = kAlgo == 2 ? 1 : 3;
+    constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= st.total_spans) return;
@@ -850,7 +1077,10 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
     locate(st, g, si, off);
     const uint64_t len = st.lens[si];
     const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
-    const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6};
+    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * 64 * 24 : 16];
+    const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
+                kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
+                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * 64 * 24 : 0)};
     uint64_t c = 0;
     if (off != 0) {  // warm-up start as walk_kernel (max-length grid)
         c = off > wp.warm ? off - wp.warm : 0;
@@ -939,7 +1169,7 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
 template <int kAlgo>
 __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
     if (ws.gate && *ws.gate == 0) return;  // the previous round settled everything
-    constexpr uint32_t nbm = kAlgo == 2 ? 1 : 3;
+    constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
     __shared__ uint64_t nbuf[4 * kNew];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -952,7 +1182,10 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     if (ws.Es[g] == x) return;
     const uint64_t len = st.lens[si];
     const uint64_t span = 1ull << st.span_log2;
-    const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6};
+    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * 64 * 24 : 16];
+    const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
+                kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
+                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * 64 * 24 : 0)};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
     uint64_t gg = g;
     for (uint32_t k = 0;; ++k) {
@@ -971,6 +1204,38 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
         x = xo;
         ++gg;
         off += span;
+    }
+}
+
+// serial_kernel with a wave per stream (wave-cooperative re-walks).  The exit
+// of a segment this pass re-walked is carried in a register (lane 0 wrote it;
+// the other lanes do not read it back from memory).
+template <int kAlgo>
+__global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
+    constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
+    __shared__ uint64_t nbuf[4 * kNew];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t si = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (si >= st.n) return;
+    const uint64_t g0 = st.span_base[si], g1 = st.span_base[si + 1];
+    const uint64_t len = st.lens[si];
+    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * 64 * 24 : 16];
+    const WBm B{wp.bm + g0 * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
+                kAlgo == 5 ? wp.jt + g0 * (uint64_t)wp.seg_words * 24 : nullptr,
+                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * 64 * 24 : 0)};
+    uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
+    uint64_t xprev = 0;
+    bool have = false;
+    for (uint64_t g = max(g0 + 1, (uint64_t)ws.flags[2]); g < g1; ++g) {
+        const uint64_t x = have ? xprev : ws.X[g - 1];
+        have = false;
+        if (ws.E[g] == x) continue;
+        const uint64_t off = (g - g0) << st.span_log2;
+        const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
+        uint64_t xo;
+        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, wp, ws, nb, lane, xo);
+        xprev = xo;
+        have = true;
     }
 }
 
@@ -1026,6 +1291,55 @@ __device__ __forceinline__ void for_chunks(const uint8_t *base, uint64_t len, ui
     }
 }
 
+// UltraCDC predicate bits of one 64-position word from its bytes w[4..19]
+// (w[0..3] = the 16 bytes before, w[20..23] = the 16 after): bitmaps 0
+// (dist & MASK_S == 0), 1 (dist & MASK_L == 0), 2 (8-byte repeat).
+__device__ __forceinline__ void ultra_word(const uint32_t (&w)[24], uint64_t *out) {
+    // equality bits E(i) = (b[i] == b[i-8]) for i = p0 .. p0+71 (first:
+    // w is dead after the popcounts, which keeps the kernel's VGPRs low)
+    uint32_t e[3] = {0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+        const uint32_t x = w[k + 4] ^ w[k + 2];
+        const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // bit 7 of each zero byte
+        const uint32_t nib = (((z >> 7) * 0x204081u) >> 21) & 0xFu;
+        e[k >> 3] |= nib << (4 * (k & 7));
+    }
+    constexpr uint32_t pat4 = 0x01010101u * CDC_ULTRA_PATTERN;
+    uint32_t cw[18];  // per-byte popcounts of words 2..19 (positions p0-8 .. p0+63)
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+        uint32_t x = w[k + 2] ^ pat4;
+        x = x - ((x >> 1) & 0x55555555u);
+        x = (x & 0x33333333u) + ((x >> 2) & 0x33333333u);
+        cw[k] = (x + (x >> 4)) & 0x0F0F0F0Fu;
+    }
+    // T(j) = dist(p0+j) + 128 j: one byte-select add per position (bytes
+    // of 128 + c(q) - c(q-8), no borrows); the masks test bits < 7 only.
+    uint32_t T = ((cw[0] * 0x01010101u) >> 24) + ((cw[1] * 0x01010101u) >> 24);  // dist(p0)
+    uint32_t hs0 = 0, hs1 = 0, hl0 = 0, hl1 = 0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        const uint32_t bs = min(T & (uint32_t)CDC_ULTRA_MASK_S, 1u);  // 0 = hit
+        const uint32_t bl = min(T & (uint32_t)CDC_ULTRA_MASK_L, 1u);
+        if (j < 32) {
+            hs0 |= bs << j;
+            hl0 |= bl << j;
+        } else {
+            hs1 |= bs << (j - 32);
+            hl1 |= bl << (j - 32);
+        }
+        const uint32_t dw = (cw[2 + (j >> 2)] | 0x80808080u) - cw[j >> 2];
+        T += __builtin_amdgcn_ubfe(dw, 8 * (j & 3), 8);
+    }
+    typedef unsigned __int128 u128;
+    const u128 E = ((u128)e[2] << 64) | ((u128)e[1] << 32) | e[0];
+    const u128 a2 = E & (E >> 1), a4 = a2 & (a2 >> 2), a8 = a4 & (a4 >> 4);
+    out[0] = ~(((uint64_t)hs1 << 32) | hs0);
+    out[1] = ~(((uint64_t)hl1 << 32) | hl0);
+    out[2] = (uint64_t)a8;
+}
+
 template <int kAlgo>
 __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, const WalkParams wp) {
     __shared__ uint64_t tab[768];
@@ -1058,6 +1372,55 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
         // window [i-47, i], exactly the digest cut_rabin tests.
         const uint64_t f0 = p0 >= CDC_RABIN_WINDOW ? p0 - CDC_RABIN_WINDOW : 0;
         uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0;  // chunks 48, 32, 16 bytes back
+        if (wp.rabin_mask <= 0xFFFFFFFFull && wp.rabin_shift >= 32 && (p0 & 63) == 0) {
+            // The digest as two dwords (deg < 64): per byte one v_alignbit
+            // for the 8-bit shift of the high dword, one v_lshl_or for the
+            // low one, the two table XORs, and a 32-bit test; the 48-byte
+            // warm-up runs without tests, then whole 64-position words.
+            const uint32_t rmask = (uint32_t)wp.rabin_mask, tsh = wp.rabin_shift - 32;
+            uint32_t lo = 0, hi = 0;
+            auto step16 = [&](const uint4 &cur, const uint4 &old, uint32_t &bits, int sh, bool test) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint64_t o = T.out[byte_of(old, j)];
+                    lo ^= (uint32_t)o;
+                    hi ^= (uint32_t)(o >> 32);
+                    const uint64_t m = T.mod[hi >> tsh];
+                    hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
+                    lo = ((lo << 8) | byte_of(cur, j)) ^ (uint32_t)m;
+                    if (test) bits |= min(lo & rmask, 1u) << (sh + j);
+                }
+            };
+            uint32_t dummy = 0;
+            for (uint64_t a = f0; a < p0; a += 16) {
+                const uint4 cur = load16_guarded(base, a, len);
+                step16(cur, c0, dummy, 0, false);
+                c0 = c1;
+                c1 = c2;
+                c2 = cur;
+            }
+            uint4 n0 = load16_guarded(base, p0, len), n1 = load16_guarded(base, p0 + 16, len);
+            uint4 n2 = load16_guarded(base, p0 + 32, len), n3 = load16_guarded(base, p0 + 48, len);
+            for (uint64_t a = p0; a < p1; a += 64) {
+                const uint4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+                if (a + 64 < p1) {
+                    n0 = load16_guarded(base, a + 64, len);
+                    n1 = load16_guarded(base, a + 80, len);
+                    n2 = load16_guarded(base, a + 96, len);
+                    n3 = load16_guarded(base, a + 112, len);
+                }
+                uint32_t b0 = 0, b1 = 0;
+                step16(q0, c0, b0, 0, true);
+                step16(q1, c1, b0, 16, true);
+                step16(q2, c2, b1, 0, true);
+                step16(q3, q0, b1, 16, true);
+                c0 = q1;
+                c1 = q2;
+                c2 = q3;
+                out[(a - p0) >> 6] = ~(((uint64_t)b1 << 32) | b0);  // bit set = window hit
+            }
+            continue;
+        }
         uint64_t d = 0, acc = 0;
         for_chunks(base, len, f0, p1, [&](const uint4 &cur, uint64_t a) {
 #pragma unroll
@@ -1080,6 +1443,28 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
         });
         if ((p1 - p0) & 63) out[(p1 - p0) >> 6] = acc;
     } else if constexpr (kAlgo == 4) {
+      if (fine) {
+        // One 64-position word per lane, on 32-bit words: per-byte popcounts
+        // c(i) = popcount(b[i] ^ 0xAA) by SWAR, dist(q) = sum c(q-8 .. q-1)
+        // kept as a running sum (+c(q) - c(q-8) per position); the repeat
+        // bit of q = bytes q .. q+7 all equal the byte 8 before them, from
+        // per-byte equality bits (SWAR zero-byte test of w[k] ^ w[k-2]) and
+        // three shift-ANDs.  Words: w[0..3] = [p0-16, p0), w[4..19] = the
+        // lane's 64 bytes, w[20..23] = [p0+64, p0+80); bytes past the stream
+        // end read 0 (as load16_guarded).
+        uint32_t w[24];
+        {
+            const uint4 a = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
+            w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint4 v = load16_guarded(base, p0 + 16 * k, len);
+                w[4 + 4 * k] = v.x; w[5 + 4 * k] = v.y; w[6 + 4 * k] = v.z; w[7 + 4 * k] = v.w;
+            }
+        }
+        ultra_word(w, out);
+        continue;
+      }
         // dist(q) = popcount of the 8 bytes before q ^ 0xAA..; repeat(q) =
         // the 8 bytes at q equal the 8 before.  A chunk's positions are
         // evaluated when the chunk after it arrives (bytes [a-16, a+32) in W).
@@ -1158,6 +1543,118 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             prev = cur;
         });
     }
+    }
+}
+
+// Rabin's bitmap pass with replicated tables: 4 segments (waves) per block
+// share 8 replicas of the mod / out tables (32 KiB of LDS; lane l reads
+// replica l & 7, entry e at (8 e + r) * 8, so at most 4 lanes of a 32-lane
+// bank group share a replica).  PMC of the single-copy tables showed 4x LDS
+// cycles in bank conflicts (profiles/r03_walk); 8 replicas with 4 waves per
+// block measured 610 us per GiB, 32 conflict-free replicas with 16 waves per
+// block (128 KiB, one block per CU) 687 us.  Lane l hashes 1/64 of its wave's segment from a
+// 48-byte warm-up (as bits_kernel<2>), the digest as two dwords.
+constexpr int kRabinReps = 8;
+constexpr int kRabinWaves = 4;  // segments per block (32 KiB of tables shared by 4 waves)
+
+__global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTable st, const WalkParams wp) {
+    __shared__ uint64_t rt[2 * 256 * kRabinReps];  // [table][entry][replica]: mod, out
+    for (int i = threadIdx.x; i < 2 * 256 * kRabinReps; i += 64 * kRabinWaves) {
+        const int t = i / (256 * kRabinReps), e = (i / kRabinReps) & 255;
+        rt[i] = wp.tabs[t * 256 + e];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * kRabinWaves + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    const uint64_t *tmod = rt + (lane & (kRabinReps - 1)), *tout = tmod + 256 * kRabinReps;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint8_t *base = st.ptrs[si];
+    const uint64_t w = (1ull << st.span_log2) >> 6;  // bytes per lane (a multiple of 64)
+    const uint64_t p0 = off + lane * w;
+    if (p0 >= len) return;
+    const uint64_t p1 = min(p0 + w, len);
+    uint64_t *out = wp.bm + (g * wp.seg_words + lane * (w >> 6));
+    const uint32_t rmask = (uint32_t)wp.rabin_mask, tsh = wp.rabin_shift - 32;
+    uint32_t lo = 0, hi = 0;
+    auto step16 = [&](const uint4 &cur, const uint4 &old, uint32_t &bits, int sh, bool test) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t o = tout[byte_of(old, j) * kRabinReps];
+            lo ^= (uint32_t)o;
+            hi ^= (uint32_t)(o >> 32);
+            const uint64_t m = tmod[(hi >> tsh) * kRabinReps];
+            hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
+            lo = ((lo << 8) | byte_of(cur, j)) ^ (uint32_t)m;
+            if (test) bits |= min(lo & rmask, 1u) << (sh + j);
+        }
+    };
+    uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0;  // chunks 48, 32, 16 bytes back
+    uint32_t dummy = 0;
+    for (uint64_t a = p0 >= CDC_RABIN_WINDOW ? p0 - CDC_RABIN_WINDOW : p0; a < p0; a += 16) {
+        const uint4 cur = load16_guarded(base, a, len);
+        step16(cur, c0, dummy, 0, false);
+        c0 = c1;
+        c1 = c2;
+        c2 = cur;
+    }
+    uint4 n0 = load16_guarded(base, p0, len), n1 = load16_guarded(base, p0 + 16, len);
+    uint4 n2 = load16_guarded(base, p0 + 32, len), n3 = load16_guarded(base, p0 + 48, len);
+    for (uint64_t a = p0; a < p1; a += 64) {
+        const uint4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+        if (a + 64 < p1) {
+            n0 = load16_guarded(base, a + 64, len);
+            n1 = load16_guarded(base, a + 80, len);
+            n2 = load16_guarded(base, a + 96, len);
+            n3 = load16_guarded(base, a + 112, len);
+        }
+        uint32_t b0 = 0, b1 = 0;
+        step16(q0, c0, b0, 0, true);
+        step16(q1, c1, b0, 16, true);
+        step16(q2, c2, b1, 0, true);
+        step16(q3, q0, b1, 16, true);
+        c0 = q1;
+        c1 = q2;
+        c2 = q3;
+        out[(a - p0) >> 6] = ~(((uint64_t)b1 << 32) | b0);  // bit set = window hit
+    }
+}
+
+// UltraCDC's bitmap pass: 4 segments (waves) per block, lane per 64-position
+// word, the wave sweeping its segment 4 KiB per step with the next step's
+// six 16-byte loads in flight while ultra_word runs on the current one.
+__device__ __forceinline__ void ultra_load(uint4 (&v)[6], const uint8_t *base, uint64_t len, uint64_t p0) {
+    v[0] = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[1 + k] = load16_guarded(base, p0 + 16 * k, len);
+}
+
+__global__ __launch_bounds__(256) void ubits_kernel(const StreamTable st, const WalkParams wp) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    const uint64_t len = st.lens[si];
+    const uint8_t *base = st.ptrs[si];
+    const uint32_t reps = (uint32_t)((1ull << st.span_log2) >> 12);
+    uint4 nx[6];
+    ultra_load(nx, base, len, off + 64ull * lane);
+    for (uint32_t it = 0; it < reps; ++it) {
+        const uint64_t lidx = (uint64_t)it * 64 + lane;
+        const uint64_t p0 = off + lidx * 64;
+        if (p0 >= len) return;
+        uint32_t w[24];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            w[4 * k] = nx[k].x; w[4 * k + 1] = nx[k].y; w[4 * k + 2] = nx[k].z; w[4 * k + 3] = nx[k].w;
+        }
+        if (it + 1 < reps && p0 + 4096 < len) ultra_load(nx, base, len, p0 + 4096);
+        ultra_word(w, wp.bm + (g * wp.seg_words + lidx) * 3);
     }
 }
 
@@ -1411,11 +1908,17 @@ hipError_t dispatch(int which, const StreamTable &st, const WalkParams &wp, cons
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
     if (!st.total_spans || !wp.nbm) return hipSuccess;
     const unsigned blocks = (unsigned)st.total_spans;
-    if (wp.algo == 2) bits_kernel<2><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    if (wp.algo == 2 && wp.rabin_mask <= 0xFFFFFFFFull && wp.rabin_shift >= 32 && st.span_log2 >= 12)
+        rbits_kernel<<<(unsigned)((st.total_spans + kRabinWaves - 1) / kRabinWaves), 64 * kRabinWaves, 0, s>>>(st, wp);
+    else if (wp.algo == 2) bits_kernel<2><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    else if (wp.algo == 4 && wp.bits_fine && st.span_log2 >= 12)
+        ubits_kernel<<<(unsigned)((st.total_spans + 3) / 4), 256, 0, s>>>(st, wp);
     else if (wp.algo == 4) bits_kernel<4><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 5) bits_kernel<5><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 6) bits_kernel<6><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else return hipErrorInvalidValue;
+    if (wp.algo == 5 && wp.wave && wp.jt && wp.seg_words >= 64)  // LeapCDC word tables
+        jtab_kernel<<<(unsigned)((st.total_spans + 3) / 4), 256, 0, s>>>(st, wp);
     return hipGetLastError();
 }
 
@@ -1428,9 +1931,11 @@ hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t
 }
 
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
-    if (wp.wave && wp.nbm && st.total_spans && (wp.algo == 2 || wp.algo == 4)) {
+    if (wp.wave && wp.nbm && st.total_spans) {
         const unsigned blocks = (unsigned)((st.total_spans + 3) / 4);
         if (wp.algo == 2) wwalk_kernel<2><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else if (wp.algo == 5) wwalk_kernel<5><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else if (wp.algo == 6) wwalk_kernel<6><<<blocks, 256, 0, s>>>(st, wp, ws);
         else wwalk_kernel<4><<<blocks, 256, 0, s>>>(st, wp, ws);
         return hipGetLastError();
     }
@@ -1443,9 +1948,11 @@ hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkSta
     if (e != hipSuccess) return e;
     e = hipMemcpyAsync(ws.Es, ws.E, st.total_spans * 8, hipMemcpyDeviceToDevice, s);
     if (e != hipSuccess) return e;
-    if (wp.wave && wp.nbm && (wp.algo == 2 || wp.algo == 4)) {
+    if (wp.wave && wp.nbm) {
         const unsigned blocks = (unsigned)((st.total_spans + 3) / 4);
         if (wp.algo == 2) wfix_kernel<2><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else if (wp.algo == 5) wfix_kernel<5><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else if (wp.algo == 6) wfix_kernel<6><<<blocks, 256, 0, s>>>(st, wp, ws);
         else wfix_kernel<4><<<blocks, 256, 0, s>>>(st, wp, ws);
         return hipGetLastError();
     }
@@ -1453,6 +1960,14 @@ hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkSta
 }
 
 hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
+    if (wp.wave && wp.nbm && st.total_spans) {
+        const unsigned blocks = (unsigned)((st.n + 3) / 4);
+        if (wp.algo == 2) wserial_kernel<2><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else if (wp.algo == 5) wserial_kernel<5><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else if (wp.algo == 6) wserial_kernel<6><<<blocks, 256, 0, s>>>(st, wp, ws);
+        else wserial_kernel<4><<<blocks, 256, 0, s>>>(st, wp, ws);
+        return hipGetLastError();
+    }
     return dispatch(2, st, wp, ws, s);
 }
 

@@ -60,6 +60,10 @@ struct WalkParams {
     uint32_t *vseg;           // [vcap] its stream's first segment (for find_cand)
     uint64_t *vnext;          // [vcap] next start after a chunk starting there
     uint32_t *vidx;           // [vcap] slot of that next start (candidate, kVirt | v, kNoCand)
+    // LeapCDC wave walks: per 64-position word w, the leap orbit of each
+    // entry candidate 64 w + e (e < 24) through the word, jt[w * 24 + e]:
+    // < 24 = its entry into word w + 1, >= 64 = accepted at 64 w + (v - 64).
+    uint8_t *jt;
 };
 
 constexpr uint32_t kNoCand = 0xFFFFFFFFu;
