@@ -177,7 +177,6 @@ class Engine {
     static constexpr size_t kRingSlot = size_t(4) << 20;
     static constexpr size_t kWriteWindow = size_t(256) << 20;
     static constexpr size_t kRingDirect = size_t(16) << 20;  // chunk_data above this: pageable hipMemcpyAsync
-    static constexpr size_t kUploadPiece = size_t(512) << 10;  // chunk_data: copy of piece k+1 overlaps DMA k
     void *h_ring_ = nullptr;
     std::unique_ptr<CopyPool> pool_;
     hipEvent_t ring_ev_[kRingSlots] = {};

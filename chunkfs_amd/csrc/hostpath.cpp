@@ -94,7 +94,7 @@ void CopyPool::run(unsigned id) {
 
 void CopyPool::copy(void *dst, const void *src, size_t n) {
     const unsigned helpers = (unsigned)th_.size();
-    if (n < (size_t(1) << 20) || helpers == 0) {  // not worth a hand-off
+    if (n < (size_t(256) << 10) || helpers == 0) {  // not worth a hand-off
         std::memcpy(dst, src, n);
         return;
     }
@@ -193,10 +193,9 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
     // stages with several threads (measured 51 vs 31 GiB/s for the single-
     // thread ring on 1 GiB).
     if (len <= kRingDirect) {
-        // (up to 2 MiB: 512 KiB pieces copied by this thread, so that the copy
-        // of one overlaps the DMA of the previous; larger: 4 MiB pieces copied
-        // by the pool)
-        rc = upload(data, len, d_data_, own_stream_, len <= (size_t(2) << 20) ? kUploadPiece : kRingSlot);
+        // (4 MiB pieces, each copied by the pool and moved by one DMA: one
+        // 1 MiB call is one hand-off and one hipMemcpyAsync)
+        rc = upload(data, len, d_data_, own_stream_, kRingSlot);
         if (rc) return rc;
     } else {
         HIP_TRY(hipMemcpyAsync(d_data_, data, len, hipMemcpyHostToDevice, own_stream_));
