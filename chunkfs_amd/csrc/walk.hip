@@ -8,10 +8,15 @@
 // the reference's crate (cdc-chunkers 0.1.3, absent offline).
 //
 // Kernels, one launch each, all on the handle's stream:
-//   walk_kernel    lane per segment: warm-up walk, then the segment's starts
-//   fix_kernel     lane per segment: re-walk where entry != predecessor exit,
-//                  running ahead into unscheduled successors
-//   serial_kernel  one lane: in-order re-walk from the lowest changed segment
+//   *bits_kernel   per-position predicate bitmaps (data-parallel pass)
+//   jtab_kernel    LeapCDC: per-word orbit tables
+//   wwalk_kernel   wave per segment: warm-up walk, then the segment's starts
+//                  (bitmap mode; walk_kernel = lane per segment, byte mode and
+//                  the CHUNKFS_AMD_WAVE=0 A/B path)
+//   wfix_kernel    re-walk where entry != predecessor exit, running ahead
+//                  into unscheduled successors (fix_kernel: lane version)
+//   wserial_kernel wave per stream: in-order re-walk from the lowest changed
+//                  segment (serial_kernel: lane per stream)
 //   sum/scan/emit  block sums of N -> block prefix -> per-segment prefix and
 //                  the Chunk{offset,length} output; first[] per stream
 #include "walk.hpp"

@@ -2,7 +2,8 @@
 // (reference src/chunkers/{rabin,ultra,leap,seq}.rs; DESIGN.md "Segment walk").
 //
 // Every stream of the batch is cut into segments of 2^seg_log2 bytes (a chunk
-// may span whole segments: they then hold no start, E = X).  One lane owns one segment and runs the
+// may span whole segments: they then hold no start, E = X).  One wave (bitmap
+// mode; one lane in byte mode) owns one segment and runs the
 // algorithm's exact byte-serial cut rule (the same rule as oracle/cdc_oracle.c)
 // from a warm-up start `warm` bytes before the segment, recording the chunk
 // starts that fall inside it.  A chain from the warm-up start usually merges
