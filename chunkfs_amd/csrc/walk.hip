@@ -954,11 +954,25 @@ __device__ __forceinline__ uint32_t leap_step(uint64_t plo, uint64_t phi, uint64
     return 0;
 }
 
-// Word tables: wave per segment (4 per block), lane per word.
+// Word tables: wave per segment (4 per block), lane per word, in two passes
+// over the word's 64 candidates (unrolled, no divergence):
+//  1. forward: the next candidate after each one.  With the last primary
+//     failing window lz before x kept incrementally, a primary failure leaps
+//     to lz + 25 (the leap 3 + j of cut_leap_bits), else the secondary windows
+//     x-23, x-24 leap 2 / 1, else x is accepted.  Packed 4 per VGPR.
+//  2. backward: the orbit result of each candidate, res[x] = accepted (64 + x),
+//     the entry into the next word (next - 64), or res[next], kept in the
+//     lane's LDS slot (68-byte stride: the 64 lanes' slots start on 64
+//     different banks).
+// Entries 0..23 are res[0..23].
+constexpr uint32_t kJSlot = 68;
+
 __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const WalkParams wp) {
+    __shared__ __attribute__((aligned(16))) uint8_t res_lds[256 * kJSlot];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= st.total_spans) return;
+    uint8_t *res = res_lds + threadIdx.x * kJSlot;
     uint32_t si;
     uint64_t off;
     locate(st, g, si, off);
@@ -967,39 +981,46 @@ __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const W
     const uint64_t *bm = wp.bm + base * 2;
     uint8_t *jt = wp.jt + base * 24;
     const uint64_t nk = (len + 63) >> 6;
+    constexpr int kP = (int)CDC_LEAP_PRIMARY;
     for (uint32_t r = 0; r < wp.seg_words / 64; ++r) {
         const uint64_t w = (off >> 6) + (uint64_t)r * 64 + lane;
         if (w >= nk) return;
         const uint64_t phi = bm[2 * w], shi = bm[2 * w + 1];
         const uint64_t plo = w ? bm[2 * w - 2] : 0ull, slo = w ? bm[2 * w - 1] : 0ull;
-        // Entry e's orbit usually lands on entry e-1's within a leap or two
-        // (consecutive candidates share their nearest failing window): `vis`
-        // holds the positions of the word whose orbit result is `pv`, and an
-        // orbit that reaches one of them takes that result.
-        uint32_t o[6] = {0, 0, 0, 0, 0, 0};
-        uint64_t vis = 0;
-        uint32_t pv = 0;
+        const uint64_t zlo = ~plo, zhi = ~phi;  // primary failing windows
+        // lz: the last failing primary window before candidate 0 (offsets
+        // relative to the word; -1000 = none in reach)
+        int lz = zlo ? (63 - (int)__builtin_clzll(zlo)) - 64 : -1000;
+        uint32_t nx[16];
 #pragma unroll
-        for (int e = 0; e < 24; ++e) {
-            uint32_t x = (uint32_t)e, v;
-            uint64_t mine = 0;
-            bool merged = false;
-            for (;;) {
-                if ((vis >> x) & 1) { v = pv; merged = true; break; }
-                mine |= 1ull << x;
-                const uint32_t l = leap_step(plo, phi, slo, shi, x);
-                if (!l) { v = 64 + x; break; }
-                x += l;
-                if (x >= 64) { v = x - 64; break; }
+        for (int x = 0; x < 64; ++x) {
+            if (x > 0) {
+                const bool f = x - 1 < 32 ? ((uint32_t)zhi >> (x - 1)) & 1 : ((uint32_t)(zhi >> 32) >> (x - 33)) & 1;
+                lz = f ? x - 1 : lz;
             }
-            vis = merged ? vis | mine : mine;
-            pv = v;
-            o[e >> 2] |= v << (8 * (e & 3));
+            // secondary windows x-23, x-24 (offsets in [-24, 40])
+            const int a = x - kP - 1, b = x - kP - 2;
+            const bool s23 = a >= 0 ? (shi >> a) & 1 : (slo >> (64 + a)) & 1;
+            const bool s24 = b >= 0 ? (shi >> b) & 1 : (slo >> (64 + b)) & 1;
+            const uint32_t nxt = lz >= x - kP ? (uint32_t)(lz + (int)CDC_LEAP_WINDOWS + 1)
+                                : !s23 ? (uint32_t)(x + 2) : !s24 ? (uint32_t)(x + 1) : 255u;
+            if ((x & 3) == 0) nx[x >> 2] = nxt;
+            else nx[x >> 2] |= nxt << (8 * (x & 3));
         }
+#pragma unroll
+        for (int x = 63; x >= 0; --x) {
+            const uint32_t n = (nx[x >> 2] >> (8 * (x & 3))) & 0xFFu;
+            uint32_t v;
+            if (n == 255u) v = 64u + (uint32_t)x;
+            else if (n >= 64u) v = n - 64u;
+            else v = res[n];
+            res[x] = (uint8_t)v;
+        }
+        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(res);
         uint64_t *d = reinterpret_cast<uint64_t *>(jt + w * 24);
-        d[0] = ((uint64_t)o[1] << 32) | o[0];
-        d[1] = ((uint64_t)o[3] << 32) | o[2];
-        d[2] = ((uint64_t)o[5] << 32) | o[4];
+        d[0] = ((uint64_t)r32[1] << 32) | r32[0];
+        d[1] = ((uint64_t)r32[3] << 32) | r32[2];
+        d[2] = ((uint64_t)r32[5] << 32) | r32[4];
     }
 }
 
