@@ -685,16 +685,27 @@ int Engine::init_walk(const uint32_t *seq) {
     // Wave walks: 128 KiB (Rabin, Leap) / 256 KiB segments, 8 avg warm-up
     // (profiles/r03_walk/r03w_walk_seg_sweep.txt: a wave walks thousands of
     // positions per step, so fewer, longer segments cut the warm-up share).
-    seg_log2_ = !wp.wave ? 15 : algo_ == CDC_ALGO_RABIN || algo_ == CDC_ALGO_LEAP ? 17 : 18;
+    // Warm-up, in averages: chains from an arbitrary start merge within a few
+    // content-defined cuts.  Lane walks: 8 avg, SeqCDC 16
+    // (profiles/r02ag_walk_warm_sweep.log).  Wave walks: Rabin 8, UltraCDC and
+    // SeqCDC 16, LeapCDC 24 (its chains merge slowest; the fix-up rounds a
+    // shorter warm-up leaves cost more than the walk it saves,
+    // profiles/r03_walk/r03ab_walk_warm_ahead_sweep.txt).
+    uint64_t warm_mult = !wp.wave ? (algo_ == CDC_ALGO_SEQ ? 16 : 8)
+                       : algo_ == CDC_ALGO_RABIN ? 8 : algo_ == CDC_ALGO_LEAP ? 24 : 16;
+    // Segments: lane walks 32 KiB whatever the average (profiles/r02ak).  Wave
+    // walks: at least 128 KiB (Rabin) / 256 KiB and at least the warm-up, so
+    // that the warm-up stays a fraction of each wave's walk (a wave walks
+    // thousands of positions per step; r03w_walk_seg_sweep.txt), up to 4 MiB.
+    seg_log2_ = !wp.wave ? 15 : algo_ == CDC_ALGO_RABIN ? 17 : 18;
+    if (wp.wave) {
+        const uint32_t wl = ceil_log2(warm_mult * avg_);
+        if (wl > seg_log2_) seg_log2_ = wl < 22 ? wl : 22;
+    }
     // The per-segment start list holds segment/min + 2 entries: keep it <= ~4k
     // (tiny min), and segments >= 4 KiB.
     const uint32_t lmin = 63 - (uint32_t)__builtin_clzll((uint64_t)min_) + 12;
     if (seg_log2_ > lmin) seg_log2_ = lmin < 12 ? 12 : lmin;
-    // SeqCDC chains (jumps skip most positions) merge more slowly: 16 avg for
-    // the lane walks (profiles/r02ag_walk_warm_sweep.log: 226 -> 241 GiB/s;
-    // the other rules gain nothing from a longer warm-up); 8 avg for all
-    // wave walks.
-    uint64_t warm_mult = algo_ == CDC_ALGO_SEQ && !wp.wave ? 16 : 8;
     if (const char *w = std::getenv("CHUNKFS_AMD_WALK")) {
         unsigned a = 0, b = 0;
         if (std::sscanf(w, "%u,%u", &a, &b) == 2 && a >= 10 && a <= 30) {
@@ -736,6 +747,7 @@ int Engine::init_walk(const uint32_t *seq) {
     if (!wp.nbm) wp.links = 0;  // links are computed over the bitmaps
     if (wp.wave) wp.links = 0;  // the wave walks replace link mode
     wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);
+    wp.piece_log2 = seg_log2_ < 15 ? seg_log2_ : 15;  // data-parallel passes: 32 KiB pieces
     wp.bm = nullptr;
     // Tables: Rabin mod/out (appending a byte; sliding one out of the window),
     // LeapCDC window-hash table.

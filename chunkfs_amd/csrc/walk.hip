@@ -40,6 +40,27 @@ __device__ __forceinline__ void locate(const StreamTable &st, uint64_t g, uint32
     off = (g - st.span_base[lo]) << st.span_log2;
 }
 
+// The data-parallel passes (bitmaps, Leap tables) run over pieces of
+// 2^wp.piece_log2 bytes, so their parallelism does not shrink when the walk
+// segments grow.  Piece q: segment g, stream si, stream offset off, and the
+// index of its first 64-position word in the segment-major bitmap arrays.
+struct Piece {
+    uint64_t g, off, wbase;
+    uint32_t si;
+};
+
+__device__ __forceinline__ bool piece_of(const StreamTable &st, const WalkParams &wp, uint64_t q, Piece &p) {
+    const uint32_t k = st.span_log2 - wp.piece_log2;
+    p.g = q >> k;
+    if (p.g >= st.total_spans) return false;
+    uint64_t off;
+    locate(st, p.g, p.si, off);
+    const uint64_t sub = q & ((1ull << k) - 1);
+    p.off = off + (sub << wp.piece_log2);
+    p.wbase = p.g * wp.seg_words + (sub << (wp.piece_log2 - 6));
+    return true;
+}
+
 // Byte reader over one stream: a per-lane window of kWin bytes in LDS.  A
 // lane that steps outside its window makes EVERY active lane of the wave
 // re-centre its own window at its current position in the same refill (one
@@ -970,19 +991,18 @@ constexpr uint32_t kJSlot = 68;
 __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const WalkParams wp) {
     __shared__ __attribute__((aligned(16))) uint8_t res_lds[256 * kJSlot];
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= st.total_spans) return;
+    Piece pc;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), pc)) return;
     uint8_t *res = res_lds + threadIdx.x * kJSlot;
-    uint32_t si;
-    uint64_t off;
-    locate(st, g, si, off);
+    const uint32_t si = pc.si;
+    const uint64_t off = pc.off;
     const uint64_t len = st.lens[si];
     const uint64_t base = st.span_base[si] * (uint64_t)wp.seg_words;
     const uint64_t *bm = wp.bm + base * 2;
     uint8_t *jt = wp.jt + base * 24;
     const uint64_t nk = (len + 63) >> 6;
     constexpr int kP = (int)CDC_LEAP_PRIMARY;
-    for (uint32_t r = 0; r < wp.seg_words / 64; ++r) {
+    for (uint32_t r = 0; r < (1u << (wp.piece_log2 - 12)); ++r) {
         const uint64_t w = (off >> 6) + (uint64_t)r * 64 + lane;
         if (w >= nk) return;
         const uint64_t phi = bm[2 * w], shi = bm[2 * w + 1];
@@ -1371,10 +1391,10 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     __shared__ uint64_t tab[768];
     if constexpr (kAlgo == 2 || kAlgo == 5) load_tabs(tab, wp.tabs);  // Ultra / Seq use no table
     const Tabs T{tab, tab + 256, tab + 512};
-    const uint64_t g = blockIdx.x;
-    uint32_t si;
-    uint64_t off;
-    locate(st, g, si, off);
+    Piece pc;
+    if (!piece_of(st, wp, blockIdx.x, pc)) return;
+    const uint32_t si = pc.si;
+    const uint64_t off = pc.off;
     const uint64_t len = st.lens[si];
     const uint8_t *base = st.ptrs[si];
     // Fine mode (Ultra, Leap, Seq): a lane evaluates one 64-position word at a
@@ -1382,7 +1402,7 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     // instruction covers 4 KiB contiguous and each bitmap store is coalesced;
     // the few window bytes before / after a word are re-read from cache.
     // Rabin keeps one 1/64 range per lane (its 48-byte warm-up per range).
-    const uint64_t seg_bytes = 1ull << st.span_log2;
+    const uint64_t seg_bytes = 1ull << wp.piece_log2;  // (this piece)
     const bool fine = kAlgo != 2 && wp.bits_fine != 0;
     const uint64_t w = fine ? 64 : seg_bytes >> 6;
     const uint32_t reps = fine ? (uint32_t)(seg_bytes >> 12) : 1u;
@@ -1391,7 +1411,7 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     const uint64_t p0 = off + lidx * w;
     if (p0 >= len) return;
     const uint64_t p1 = min(p0 + w, len);
-    uint64_t *out = wp.bm + (g * wp.seg_words + lidx * (w >> 6)) * wp.nbm;
+    uint64_t *out = wp.bm + (pc.wbase + lidx * (w >> 6)) * wp.nbm;
     if constexpr (kAlgo == 2) {
         // Rolling Rabin digest from 48 bytes before p0 (out bytes 0 until
         // 48 bytes are in): the digest after byte i is the fingerprint of the
@@ -1591,19 +1611,16 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * kRabinWaves + (threadIdx.x >> 6);
-    if (g >= st.total_spans) return;
+    Piece pc;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * kRabinWaves + (threadIdx.x >> 6), pc)) return;
     const uint64_t *tmod = rt + (lane & (kRabinReps - 1)), *tout = tmod + 256 * kRabinReps;
-    uint32_t si;
-    uint64_t off;
-    locate(st, g, si, off);
-    const uint64_t len = st.lens[si];
-    const uint8_t *base = st.ptrs[si];
-    const uint64_t w = (1ull << st.span_log2) >> 6;  // bytes per lane (a multiple of 64)
-    const uint64_t p0 = off + lane * w;
+    const uint64_t len = st.lens[pc.si];
+    const uint8_t *base = st.ptrs[pc.si];
+    const uint64_t w = (1ull << wp.piece_log2) >> 6;  // bytes per lane (a multiple of 64)
+    const uint64_t p0 = pc.off + lane * w;
     if (p0 >= len) return;
     const uint64_t p1 = min(p0 + w, len);
-    uint64_t *out = wp.bm + (g * wp.seg_words + lane * (w >> 6));
+    uint64_t *out = wp.bm + (pc.wbase + lane * (w >> 6));
     const uint32_t rmask = (uint32_t)wp.rabin_mask, tsh = wp.rabin_shift - 32;
     uint32_t lo = 0, hi = 0;
     auto step16 = [&](const uint4 &cur, const uint4 &old, uint32_t &bits, int sh, bool test) {
@@ -1660,14 +1677,12 @@ __device__ __forceinline__ void ultra_load(uint4 (&v)[6], const uint8_t *base, u
 
 __global__ __launch_bounds__(256) void ubits_kernel(const StreamTable st, const WalkParams wp) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (g >= st.total_spans) return;
-    uint32_t si;
-    uint64_t off;
-    locate(st, g, si, off);
-    const uint64_t len = st.lens[si];
-    const uint8_t *base = st.ptrs[si];
-    const uint32_t reps = (uint32_t)((1ull << st.span_log2) >> 12);
+    Piece pc;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), pc)) return;
+    const uint64_t off = pc.off;
+    const uint64_t len = st.lens[pc.si];
+    const uint8_t *base = st.ptrs[pc.si];
+    const uint32_t reps = (uint32_t)((1ull << wp.piece_log2) >> 12);
     uint4 nx[6];
     ultra_load(nx, base, len, off + 64ull * lane);
     for (uint32_t it = 0; it < reps; ++it) {
@@ -1680,7 +1695,7 @@ __global__ __launch_bounds__(256) void ubits_kernel(const StreamTable st, const 
             w[4 * k] = nx[k].x; w[4 * k + 1] = nx[k].y; w[4 * k + 2] = nx[k].z; w[4 * k + 3] = nx[k].w;
         }
         if (it + 1 < reps && p0 + 4096 < len) ultra_load(nx, base, len, p0 + 4096);
-        ultra_word(w, wp.bm + (g * wp.seg_words + lidx) * 3);
+        ultra_word(w, wp.bm + (pc.wbase + lidx) * 3);
     }
 }
 
@@ -1933,18 +1948,19 @@ hipError_t dispatch(int which, const StreamTable &st, const WalkParams &wp, cons
 
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
     if (!st.total_spans || !wp.nbm) return hipSuccess;
-    const unsigned blocks = (unsigned)st.total_spans;
-    if (wp.algo == 2 && wp.rabin_mask <= 0xFFFFFFFFull && wp.rabin_shift >= 32 && st.span_log2 >= 12)
-        rbits_kernel<<<(unsigned)((st.total_spans + kRabinWaves - 1) / kRabinWaves), 64 * kRabinWaves, 0, s>>>(st, wp);
+    const uint64_t pieces = st.total_spans << (st.span_log2 - wp.piece_log2);
+    const unsigned blocks = (unsigned)pieces;
+    if (wp.algo == 2 && wp.rabin_mask <= 0xFFFFFFFFull && wp.rabin_shift >= 32 && wp.piece_log2 >= 12)
+        rbits_kernel<<<(unsigned)((pieces + kRabinWaves - 1) / kRabinWaves), 64 * kRabinWaves, 0, s>>>(st, wp);
     else if (wp.algo == 2) bits_kernel<2><<<blocks, kWalkBlock, 0, s>>>(st, wp);
-    else if (wp.algo == 4 && wp.bits_fine && st.span_log2 >= 12)
-        ubits_kernel<<<(unsigned)((st.total_spans + 3) / 4), 256, 0, s>>>(st, wp);
+    else if (wp.algo == 4 && wp.bits_fine && wp.piece_log2 >= 12)
+        ubits_kernel<<<(unsigned)((pieces + 3) / 4), 256, 0, s>>>(st, wp);
     else if (wp.algo == 4) bits_kernel<4><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 5) bits_kernel<5><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 6) bits_kernel<6><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else return hipErrorInvalidValue;
-    if (wp.algo == 5 && wp.wave && wp.jt && wp.seg_words >= 64)  // LeapCDC word tables
-        jtab_kernel<<<(unsigned)((st.total_spans + 3) / 4), 256, 0, s>>>(st, wp);
+    if (wp.algo == 5 && wp.wave && wp.jt && wp.piece_log2 >= 12)  // LeapCDC word tables
+        jtab_kernel<<<(unsigned)((pieces + 3) / 4), 256, 0, s>>>(st, wp);
     return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ struct WalkParams {
     uint64_t *bm;
     uint32_t nbm;             // 0 = byte mode; Rabin 1 (hit), Ultra 3 (mask_s, mask_l, 8-byte repeat), Leap 2
     uint32_t seg_words;       // 64-bit words per segment and bitmap (segment bytes / 64)
+    uint32_t piece_log2;      // the data-parallel passes run over pieces of 2^piece_log2 bytes (<= segment)
     uint32_t bits_fine;       // bitmap pass: lane per 64-position word (Ultra, Leap, Seq)
     uint32_t ahead;           // fix-up round: segments one lane may re-walk (1 = plain Jacobi)
     uint32_t wave;            // 1: wave-cooperative walk_kernel (Rabin / UltraCDC bitmap mode)
