@@ -747,7 +747,8 @@ struct WBm {
     const uint64_t *w;
     uint64_t nk;
     const uint8_t *jt = nullptr;  // LeapCDC: the stream's word tables
-    uint8_t *lb = nullptr;        // LeapCDC: the wave's LDS slot (64 words x 24 B)
+    uint8_t *lb = nullptr;        // LeapCDC: the wave's LDS slot (kLeapSlot bytes)
+    const uint16_t *jt8 = nullptr;  // LeapCDC: the stream's block tables
     __device__ __forceinline__ uint64_t word(uint32_t nbm, uint32_t b, uint64_t k) const {
         return k < nk ? w[k * nbm + b] : 0ull;
     }
@@ -1002,11 +1003,14 @@ __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const W
     uint8_t *jt = wp.jt + base * 24;
     const uint64_t nk = (len + 63) >> 6;
     constexpr int kP = (int)CDC_LEAP_PRIMARY;
+    uint16_t *jt8 = wp.jt8 + base / 8 * 24;
     for (uint32_t r = 0; r < (1u << (wp.piece_log2 - 12)); ++r) {
-        const uint64_t w = (off >> 6) + (uint64_t)r * 64 + lane;
-        if (w >= nk) return;
-        const uint64_t phi = bm[2 * w], shi = bm[2 * w + 1];
-        const uint64_t plo = w ? bm[2 * w - 2] : 0ull, slo = w ? bm[2 * w - 1] : 0ull;
+        const uint64_t w0 = (off >> 6) + (uint64_t)r * 64;
+        if (w0 >= nk) return;  // (wave-uniform)
+        const uint64_t w = w0 + lane;
+        const bool in = w < nk;  // words past the stream end: tables never used
+        const uint64_t phi = in ? bm[2 * w] : 0ull, shi = in ? bm[2 * w + 1] : 0ull;
+        const uint64_t plo = in && w ? bm[2 * w - 2] : 0ull, slo = in && w ? bm[2 * w - 1] : 0ull;
         const uint64_t zlo = ~plo, zhi = ~phi;  // primary failing windows
         // lz: the last failing primary window before candidate 0 (offsets
         // relative to the word; -1000 = none in reach)
@@ -1036,48 +1040,83 @@ __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const W
             else v = res[n];
             res[x] = (uint8_t)v;
         }
-        const uint32_t *r32 = reinterpret_cast<const uint32_t *>(res);
-        uint64_t *d = reinterpret_cast<uint64_t *>(jt + w * 24);
-        d[0] = ((uint64_t)r32[1] << 32) | r32[0];
-        d[1] = ((uint64_t)r32[3] << 32) | r32[2];
-        d[2] = ((uint64_t)r32[5] << 32) | r32[4];
+        if (in) {
+            const uint32_t *r32 = reinterpret_cast<const uint32_t *>(res);
+            uint64_t *d = reinterpret_cast<uint64_t *>(jt + w * 24);
+            d[0] = ((uint64_t)r32[1] << 32) | r32[0];
+            d[1] = ((uint64_t)r32[3] << 32) | r32[2];
+            d[2] = ((uint64_t)r32[5] << 32) | r32[4];
+        }
+        // Block tables: lanes 8k .. 8k+7 hold the words of block w0/8 + k
+        // (w0 is a multiple of 512 words); lane 8k + j chases entries 3j ..
+        // 3j+2 through the 8 words' results in the group's LDS slots.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint8_t *grp = res_lds + (threadIdx.x & ~7u) * kJSlot;
+        const uint32_t j = lane & 7;
+        uint16_t o8[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            uint32_t x = 3 * j + q, v = 0xFFFF;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const uint32_t u = grp[t * kJSlot + x];
+                if (u >= 64) {
+                    v = 512u + 64u * t + (u - 64u);
+                    break;
+                }
+                x = u;
+            }
+            o8[q] = (uint16_t)(v == 0xFFFF ? x : v);
+        }
+        if (in) {
+            uint16_t *d8 = jt8 + (w >> 3) * 24 + 3 * j;
+            d8[0] = o8[0];
+            d8[1] = o8[1];
+            d8[2] = o8[2];
+        }
+        __builtin_amdgcn_wave_barrier();  // (the slots are rewritten next round)
     }
 }
 
-// The leap rule from candidate C (wave-uniform), words read straight from
-// the bitmaps (broadcast loads).
-__device__ __forceinline__ uint32_t leap_at(const WBm &B, uint64_t C) {
-    const uint64_t w = C >> 6;
-    const uint64_t phi = B.word(2, 0, w), shi = B.word(2, 1, w);
-    const uint64_t plo = w ? B.word(2, 0, w - 1) : 0ull, slo = w ? B.word(2, 1, w - 1) : 0ull;
-    return leap_step(plo, phi, slo, shi, (uint32_t)(C & 63));
-}
+// cut_leap_bits for one wave: leaps within the start candidate's word (its
+// four bitmap words loaded once), then the orbit through word tables up to the
+// next 512-position block boundary, block tables while a whole block is at or
+// before the bound E, and word tables up to E's word (an accepted position
+// past E, or an exit past it, means no content-defined cut: `end`).  Tables
+// are staged in the wave's LDS slot (one per lane, one load latency per
+// stage) and followed there.
+constexpr uint32_t kLeapSlot = 64 * 48 + 8 * 24;  // 64 block tables + 8 word tables
 
-// cut_leap_bits for one wave: direct leaps to the first word boundary, then
-// word tables 64 words at a time (the wave stages them in its LDS slot, one
-// word per lane, and follows the orbit through them), then direct leaps in
-// the word holding the bound (tables may accept past it).
 __device__ uint64_t wcut_leap(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
     const uint64_t E = s + end;  // candidates C <= E
     uint64_t C = s + wp.min;
-    const uint64_t wb = (C >> 6) + 1;
-    while (C < 64 * wb) {
-        if (C > E) return end;
-        const uint32_t l = leap_at(B, C);
-        if (!l) return C - s;
-        C += l;
-    }
     uint64_t w = C >> 6;
+    {
+        const uint64_t phi = B.word(2, 0, w), shi = B.word(2, 1, w);
+        const uint64_t plo = w ? B.word(2, 0, w - 1) : 0ull, slo = w ? B.word(2, 1, w - 1) : 0ull;
+        while (C < 64 * (w + 1)) {
+            if (C > E) return end;
+            const uint32_t l = leap_step(plo, phi, slo, shi, (uint32_t)(C & 63));
+            if (!l) return C - s;
+            C += l;
+        }
+    }
+    ++w;
     uint32_t e = (uint32_t)(C & 63);
-    if (E >= 63) {
-        const uint64_t wl = (E - 63) >> 6;  // last word wholly <= E
-        while (w <= wl) {
-            const uint32_t nw = (uint32_t)min(wl - w + 1, (uint64_t)64);
-            if (lane < nw) {
-                const uint64_t *src = reinterpret_cast<const uint64_t *>(B.jt + (w + lane) * 24);
-                uint64_t *dst = reinterpret_cast<uint64_t *>(B.lb + lane * 24);
+    uint16_t *b8 = reinterpret_cast<uint16_t *>(B.lb);
+    uint8_t *b1 = B.lb + 64 * 48;
+    for (;;) {
+        if (64 * w + e > E) return end;
+        if ((w & 7) == 0 && 64 * (w + 8) - 1 <= E) {
+            // whole blocks: up to 64 of them, every one at or before E
+            const uint64_t nb = min((E + 1) / 512 - w / 8, (uint64_t)64);
+            if (lane < nb) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(B.jt8 + (w / 8 + lane) * 24);
+                uint4 *dst = reinterpret_cast<uint4 *>(b8 + lane * 24);
                 dst[0] = src[0];
                 dst[1] = src[1];
                 dst[2] = src[2];
@@ -1085,22 +1124,40 @@ __device__ uint64_t wcut_leap(const WBm &B, uint64_t s, uint64_t n, const WalkPa
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t j = 0; j < nw; ++j) {
-                const uint32_t v = B.lb[j * 24 + e];
-                if (v >= 64) return 64 * (w + j) + (v - 64) - s;
+            for (uint32_t k = 0; k < nb; ++k) {
+                const uint32_t v = b8[k * 24 + e];
+                if (v >= 512) return 64 * w + (v - 512) - s;
                 e = v;
+                w += 8;
             }
-            w += nw;
-            __builtin_amdgcn_wave_barrier();  // (the slot is rewritten next round)
+            __builtin_amdgcn_wave_barrier();
+            continue;
         }
+        // word tables up to the next block boundary or E's word
+        const uint64_t wl = min(E >> 6, (w | 7));
+        const uint32_t nw = (uint32_t)(wl - w + 1);  // 1 .. 8
+        if (lane < nw) {
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(B.jt + (w + lane) * 24);
+            uint64_t *dst = reinterpret_cast<uint64_t *>(b1 + lane * 24);
+            dst[0] = src[0];
+            dst[1] = src[1];
+            dst[2] = src[2];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t k = 0; k < nw; ++k) {
+            if (64 * w + e > E) return end;
+            const uint32_t v = b1[k * 24 + e];
+            if (v >= 64) {
+                const uint64_t pos = 64 * w + (v - 64);
+                return pos <= E ? pos - s : end;
+            }
+            e = v;
+            ++w;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    C = 64 * w + e;
-    while (C <= E) {
-        const uint32_t l = leap_at(B, C);
-        if (!l) return C - s;
-        C += l;
-    }
-    return end;
 }
 
 template <int kAlgo>
@@ -1123,10 +1180,11 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
     locate(st, g, si, off);
     const uint64_t len = st.lens[si];
     const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
-    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * 64 * 24 : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
     const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
-                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * 64 * 24 : 0)};
+                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
+                kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t c = 0;
     if (off != 0) {  // warm-up start as walk_kernel (max-length grid)
         c = off > wp.warm ? off - wp.warm : 0;
@@ -1228,10 +1286,11 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     if (ws.Es[g] == x) return;
     const uint64_t len = st.lens[si];
     const uint64_t span = 1ull << st.span_log2;
-    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * 64 * 24 : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
     const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
-                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * 64 * 24 : 0)};
+                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
+                kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
     uint64_t gg = g;
     for (uint32_t k = 0;; ++k) {
@@ -1265,10 +1324,11 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
     if (si >= st.n) return;
     const uint64_t g0 = st.span_base[si], g1 = st.span_base[si + 1];
     const uint64_t len = st.lens[si];
-    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * 64 * 24 : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
     const WBm B{wp.bm + g0 * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
                 kAlgo == 5 ? wp.jt + g0 * (uint64_t)wp.seg_words * 24 : nullptr,
-                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * 64 * 24 : 0)};
+                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
+                kAlgo == 5 ? wp.jt8 + g0 * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
     uint64_t xprev = 0;
     bool have = false;

@@ -66,6 +66,10 @@ struct WalkParams {
     // entry candidate 64 w + e (e < 24) through the word, jt[w * 24 + e]:
     // < 24 = its entry into word w + 1, >= 64 = accepted at 64 w + (v - 64).
     uint8_t *jt;
+    // ... and per 512-position block b (8 words) the same through the whole
+    // block, jt8[b * 24 + e] (u16): < 24 = entry into block b + 1, >= 512 =
+    // accepted at 512 b + (v - 512).
+    uint16_t *jt8;
 };
 
 constexpr uint32_t kNoCand = 0xFFFFFFFFu;

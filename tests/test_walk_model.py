@@ -1,7 +1,8 @@
 """CPU models of the wave-walk algorithms of walk.hip (no GPU): each model
 follows the kernel's decomposition -- LeapCDC's per-word orbit tables built by
-the forward "last failing window" pass and the backward result pass
-(jtab_kernel) and the three-phase walk of wcut_leap; SeqCDC's 4096-position
+the forward "last failing window" pass and the backward result pass, the
+512-position block tables chased through 8 word tables (jtab_kernel), and
+wcut_leap's walk over them; SeqCDC's 4096-position
 windows with the carried run / opposing-pair count and the restarts a jump
 lands inside the window (wcut_seq); UltraCDC's 512-block windows with the
 LEST run carried between windows (wcut_ultra) -- and must reproduce the
@@ -89,36 +90,58 @@ def leap_step(prim, sec, c):
     return 0
 
 
-def wcut_leap(prim, sec, tabs, s, n, mn, mx):
+def block_tables(tabs):
+    """The 512-position block tables: each entry chased through 8 word tables
+    (< 24: entry into the next block, >= 512: accepted at offset v - 512)."""
+    nb = (tabs.shape[0] + 7) // 8
+    t8 = np.zeros((nb, 24), dtype=np.int64)
+    for b in range(nb):
+        for e in range(24):
+            x, v = e, None
+            for t in range(8):
+                if 8 * b + t >= tabs.shape[0]:
+                    break
+                u = int(tabs[8 * b + t, x])
+                if u >= 64:
+                    v = 512 + 64 * t + (u - 64)
+                    break
+                x = u
+            t8[b, e] = x if v is None else v
+    return t8
+
+
+def wcut_leap(prim, sec, tabs, t8, s, n, mn, mx):
+    """wcut_leap: leaps in the start candidate's word, then word tables to the
+    next block boundary, block tables while a whole block is <= E, word tables
+    up to E's word (acceptance past E = no content-defined cut)."""
     if n <= mn:
         return n
     end = min(n, mx)
     E = s + end
     c = s + mn
-    wb = (c >> 6) + 1
-    while c < 64 * wb:
+    w = c >> 6
+    while c < 64 * (w + 1):
         if c > E:
             return end
         lp = leap_step(prim, sec, c)
         if not lp:
             return c - s
         c += lp
-    w, e = c >> 6, c & 63
-    if E >= 63:
-        wl = (E - 63) >> 6
-        while w <= wl:
-            v = int(tabs[w, e])
-            if v >= 64:
-                return 64 * w + (v - 64) - s
-            e = v
-            w += 1
-    c = 64 * w + e
-    while c <= E:
-        lp = leap_step(prim, sec, c)
-        if not lp:
-            return c - s
-        c += lp
-    return end
+    w, e = w + 1, c & 63
+    while True:
+        if 64 * w + e > E:
+            return end
+        if w % 8 == 0 and 64 * (w + 8) - 1 <= E:
+            v = int(t8[w // 8, e])
+            if v >= 512:
+                return 64 * w + (v - 512) - s
+            e, w = v, w + 8
+            continue
+        v = int(tabs[w, e])
+        if v >= 64:
+            pos = 64 * w + (v - 64)
+            return pos - s if pos <= E else end
+        e, w = v, w + 1
 
 
 @pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (512, 2048, 16384), (2048, 8192, 65536)])
@@ -127,9 +150,10 @@ def test_leap_word_tables_model(sizes):
     d = oracle.splitmix64_bytes((1 << 20) + 777, 5)
     prim, sec = leap_bitmaps(d, mn, avg)
     tabs = leap_tables(prim, sec)
+    t8 = block_tables(tabs)
     got, pos = [], 0
     while pos < d.size:
-        cut = wcut_leap(prim, sec, tabs, pos, d.size - pos, mn, mx)
+        cut = wcut_leap(prim, sec, tabs, t8, pos, d.size - pos, mn, mx)
         got.append((pos, cut))
         pos += cut
     ref = oracle.cdc("leap", d, mn, avg, mx)
