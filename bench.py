@@ -155,6 +155,12 @@ class DeviceEngine:
     def timing(self):
         return self.ch.last_timing()
 
+    def timings(self, k):
+        """HIP-event timings of the last k batches (oldest first), read after
+        the timed loop from the engine's event ring (no per-step event wait
+        inside the loop; include/chunkfs_amd_debug.h)."""
+        return [self.ch.timing_back(b) for b in range(min(k, 64) - 1, -1, -1)]
+
     def sync(self):
         self.torch.cuda.synchronize()
 
@@ -178,6 +184,9 @@ class StubEngine:
     def timing(self):
         return {"scan_ms": 0.0, "total_ms": 0.0, "resolve_ms": 0.0, "fixup_iterations": 0, "walk_fallback_steps": 0}
 
+    def timings(self, k):
+        return [self.timing() for _ in range(min(k, 64))]
+
     def sync(self):
         pass
 
@@ -194,13 +203,12 @@ def timed_steps(eng, w, steps, warmup, world, red_dev):
     if world > 1:
         dist.barrier()
     eng.sync()
-    tims = []
     t0 = time.perf_counter()
     for _ in range(steps):
         first = eng.step(w)
-        tims.append(eng.timing())
     eng.sync()
     el = time.perf_counter() - t0
+    tims = eng.timings(steps)  # HIP events of the timed steps (the last <= 64 of them)
     if world > 1:
         dist.barrier()
         el = sharding.max_over_ranks(el, red_dev)

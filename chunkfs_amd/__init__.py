@@ -197,6 +197,13 @@ class Chunker:
         check(lib().cdc_last_timing(self._h, ctypes.byref(t), ctypes.sizeof(t)))
         return {f: getattr(t, f) for f, _ in cdc_timing_t._fields_}
 
+    def timing_back(self, back):
+        """Kernel times of the FastCDC batch `back` calls before the last one
+        (0 = last, <= 63; include/chunkfs_amd_debug.h cdc_debug_timing_back)."""
+        t = cdc_timing_t()
+        check(lib().cdc_debug_timing_back(self._h, back, ctypes.byref(t), ctypes.sizeof(t)))
+        return {f: getattr(t, f) for f, _ in cdc_timing_t._fields_}
+
     def set_gear(self, gear):
         g = np.ascontiguousarray(gear, dtype=np.uint64)
         assert g.shape == (256,)

@@ -30,7 +30,8 @@ EXPORTS = [
     "cdc_fill_splitmix64_device", "cdc_version", "cdc_abi_version",
 ]
 # include/chunkfs_amd_debug.h (diagnostics, not part of the drop-in boundary)
-DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy", "cdc_debug_host_stats"]
+DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy", "cdc_debug_host_stats",
+                 "cdc_debug_timing_back"]
 
 
 class CdcError(RuntimeError):
@@ -127,6 +128,8 @@ def lib():
     L.cdc_write_finish.restype = ctypes.c_int64
     L.cdc_debug_host_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), sz]
     L.cdc_debug_host_stats.restype = ctypes.c_int
+    L.cdc_debug_timing_back.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(cdc_timing_t), sz]
+    L.cdc_debug_timing_back.restype = ctypes.c_int
     L.cdc_sha256_chunks_device.argtypes = [P, P, P, sz, P, P]
     L.cdc_sha256_chunks_device.restype = ctypes.c_int
     L.cdc_chunk_and_hash.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), u8p, sz]

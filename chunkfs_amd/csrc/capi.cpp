@@ -84,6 +84,15 @@ size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n, const uint64_t *len
     return (h && lens) ? h->engine->batch_max_chunks(n, lens) : 0;
 }
 
+int cdc_debug_timing_back(cdc_handle_t *h, uint32_t back, cdc_timing_t *t, size_t t_size) {
+    if (!h || !t) return (int)bad_handle();
+    cdc_timing_t v{};
+    const int rc = h->engine->timing_back(back, v);
+    if (rc) return rc;
+    std::memcpy(t, &v, t_size < sizeof v ? t_size : sizeof v);
+    return CDC_OK;
+}
+
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size) {
     if (!h || !t) return (int)bad_handle();
     const cdc_timing_t &src = h->engine->timing();

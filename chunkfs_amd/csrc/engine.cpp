@@ -169,6 +169,8 @@ int Engine::init() {
     num_cus_ = prop.multiProcessorCount;
     HIP_TRY(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking));
     for (auto &ev : ev_) HIP_TRY(hipEventCreate(&ev));
+    for (auto &slot : tev_)
+        for (auto &ev : slot) HIP_TRY(hipEventCreate(&ev));
     HIP_TRY(hipMalloc(&d_gear_, 256 * sizeof(uint64_t)));
     HIP_TRY(hipMalloc(&d_counter_, sizeof(unsigned long long)));
     HIP_TRY(hipMemcpy(d_gear_, CHUNKFS_AMD_GEAR, 256 * sizeof(uint64_t), hipMemcpyHostToDevice));
@@ -198,6 +200,9 @@ Engine::~Engine() {
     if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     for (auto &ev : ev_)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto &slot : tev_)
+        for (auto &ev : slot)
+            if (ev) (void)hipEventDestroy(ev);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
 }
 
@@ -404,11 +409,13 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the last resolve block
     p3::Resolve rs = rs3_;
     rs.gen = ++res_gen_;
-    HIP_TRY(hipEventRecord(ev_[0], s));
+    hipEvent_t *ev = tev_[fast_batches_ % kTimeRing];
+    HIP_TRY(hipEventRecord(ev[0], s));
     HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, cur_tails_, n_tails_, num_cus_, s));
-    HIP_TRY(hipEventRecord(ev_[1], s));
+    HIP_TRY(hipEventRecord(ev[1], s));
     HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, ch3_, cp, rs, d_out, out_cap_, s));
-    HIP_TRY(hipEventRecord(ev_[2], s));
+    HIP_TRY(hipEventRecord(ev[2], s));
+    ++fast_batches_;
     // The resolve's last block writes the done word into coherent pinned
     // memory after a system-scope fence: spin on it (wakes faster than a
     // blocking stream sync) for about the batch's expected device time
@@ -460,17 +467,28 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
 const cdc_timing_t &Engine::timing() {
     if (timing_pending_) {
         timing_pending_ = false;
-        float t01 = 0, t12 = 0, t02 = 0;
-        if (hipSetDevice(device_) == hipSuccess && hipEventSynchronize(ev_[2]) == hipSuccess &&
-            hipEventElapsedTime(&t01, ev_[0], ev_[1]) == hipSuccess &&
-            hipEventElapsedTime(&t12, ev_[1], ev_[2]) == hipSuccess &&
-            hipEventElapsedTime(&t02, ev_[0], ev_[2]) == hipSuccess) {
-            timing_.scan_ms = t01;
-            timing_.resolve_ms = t12;
-            timing_.total_ms = t02;
-        }
+        (void)timing_back(0, timing_);
     }
     return timing_;
+}
+
+int Engine::timing_back(uint32_t back, cdc_timing_t &out) {
+    if (algo_ != CDC_ALGO_FASTCDC || back >= kTimeRing || back >= fast_batches_) {
+        set_error("cdc_debug_timing_back: no such FastCDC batch in the event ring");
+        return CDC_EINVAL;
+    }
+    if (&out != &timing_) out = timing_;
+    hipEvent_t *ev = tev_[(fast_batches_ - 1 - back) % kTimeRing];
+    float t01 = 0, t12 = 0, t02 = 0;
+    HIP_TRY(hipSetDevice(device_));
+    HIP_TRY(hipEventSynchronize(ev[2]));
+    HIP_TRY(hipEventElapsedTime(&t01, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&t12, ev[1], ev[2]));
+    HIP_TRY(hipEventElapsedTime(&t02, ev[0], ev[2]));
+    out.scan_ms = t01;
+    out.resolve_ms = t12;
+    out.total_ms = t02;
+    return CDC_OK;
 }
 
 int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,

@@ -94,6 +94,9 @@ class Engine {
     // seen returns before its kernels retire, and its events are read here,
     // on first request.
     const cdc_timing_t &timing();
+    // Kernel times of the FastCDC batch `back` calls before the last one
+    // (event ring, include/chunkfs_amd_debug.h).
+    int timing_back(uint32_t back, cdc_timing_t &out);
     cdc_algo_t algo() const { return algo_; }
     int device() const { return device_; }
     int fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s);
@@ -144,6 +147,11 @@ class Engine {
 
     hipStream_t own_stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+    // FastCDC batches: events (start, scan end, resolve end) in a ring of
+    // kTimeRing slots, batch k in slot k % kTimeRing.
+    static constexpr uint32_t kTimeRing = 64;
+    hipEvent_t tev_[kTimeRing][3] = {};
+    uint64_t fast_batches_ = 0;
     uint64_t *d_gear_ = nullptr;
 
     // Workspace arena (grow-only).

@@ -29,6 +29,13 @@ int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes);
  * seconds, then the chunking seconds and segment count of the current or
  * last streaming write (cdc_write_*). */
 int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n);
+/* Kernel times of the FastCDC batch `back` calls before the last one (0 = the
+ * last; up to 63 back): scan_ms, resolve_ms, total_ms of t (the other fields
+ * are the last batch's).  Each batch records its HIP events in its own slot of
+ * a 64-entry ring, so a caller timing many back-to-back batches reads them
+ * after the loop instead of waiting on each batch's events inside it.
+ * CDC_EINVAL when that batch is not in the ring. */
+int cdc_debug_timing_back(cdc_handle_t *h, uint32_t back, cdc_timing_t *t, size_t t_size);
 
 #ifdef __cplusplus
 }

@@ -259,6 +259,15 @@ def test_one_gib_stream_and_timing():
     # size-independent properties
     assert int(got[:, 1].sum()) == n
     assert (got[:-1, 1] >= sizes[0]).all() and (got[:, 1] <= sizes[2]).all()
+    # the event ring (cdc_debug_timing_back): back-to-back batches, read after
+    for _ in range(3):
+        ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+    hist = [ch.timing_back(k) for k in range(4)]
+    assert all(h["scan_ms"] > 0 and h["total_ms"] >= h["scan_ms"] for h in hist)
+    assert hist[0]["scan_ms"] == ch.last_timing()["scan_ms"]
+    from chunkfs_amd import CdcError
+    with pytest.raises(CdcError):
+        ch.timing_back(64)
 
 
 def test_config4_batch_1024_streams_of_64mib():
