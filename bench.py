@@ -10,6 +10,9 @@ Workloads:
     config 2 -- one 1 GiB stream of splitmix64(seed=1+rank) bytes per GPU,
     FastCDC 4/8/16 KiB, weak scaling: the per-GPU work is the same at every N,
     so the driver's N=1 line is the matching denominator of its 1->8 curve.
+  * `config5` sub-object (every N, unless --no-config5): config 5 -- 16 x 1 GiB
+    streams (stream i: seed 5000+i) split across the ranks, UltraCDC / LeapCDC
+    (+ Rabin, SeqCDC) at avg 2 / 8 / 64 KiB, strong scaling, no collective.
   * `config4` sub-object (every N, unless --no-config4): config 4 -- 1024
     independent 64 MiB streams (stream i: seed 1000+i) split into contiguous
     blocks across the ranks, strong scaling, no data-path collective
@@ -77,6 +80,10 @@ def parse(argv=None):
                    help="skip the one-off host-buffer (PCIe-inclusive) rates")
     p.add_argument("--config5-bytes", type=int, default=1 << 30,
                    help="bytes of the bench stream the config-5 size sweep chunks")
+    p.add_argument("--no-config5", action="store_true",
+                   help="skip the config-5 (16 GiB, walk rules at 2/8/64 KiB, strong scaling) sub-object")
+    p.add_argument("--config5-check", type=int, default=64 << 20,
+                   help="config 5: bytes of rank 0's first stream checked against the oracle")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU launcher test only
     # Multi-rank rehearsal on a box with fewer GPUs than ranks (tests only):
@@ -258,6 +265,75 @@ def config4_leg(args, eng, rank, world, red_dev):
             out["n1_value_rank0_alone"] = n1
             out["strong_scaling_efficiency"] = out["value"] / (world * n1)
     return out
+
+
+def config5_leg(args, eng, rank, world, red_dev):
+    """Config 5 (BASELINE configs[4]) at every N: 16 GiB of synthetic data as
+    16 independent 1 GiB streams (stream i: seed 5000+i) split across the ranks
+    (strong scaling, no collective), UltraCDC and LeapCDC (plus Rabin and
+    SeqCDC) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg.
+    Per (rule, sizes): one warm-up pass, then one pass bracketed by a barrier
+    and a device sync on both sides; value = 16 GiB / max-over-ranks time.
+    Rank 0 checks the chunks of its first stream that lie in the first
+    --config5-check bytes against the oracle (all but the oracle's last chunk
+    there: these rules look only forward, so a prefix's chunks but its last
+    are the stream's).  SuperCDC is not implemented (CDC_ENOTSUP)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import chunkfs_amd as cfa
+    from chunkfs_amd import sharding
+    shard = sharding.batch_shard(rank, world, 16, 1 << 30)
+    dev = eng.dev
+    bufs = []
+    for n, sd in zip(shard.lens, shard.seeds):
+        b = torch.empty(n, dtype=torch.uint8, device=dev)
+        eng._lib.check(eng._lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, 4000 + sd, None))
+        bufs.append(b)
+    torch.cuda.synchronize()
+    ptrs, lens = [b.data_ptr() for b in bufs], list(shard.lens)
+    total = sharding.sum_over_ranks(sum(lens), red_dev)
+    oracle = None
+    if rank == 0 and not args.no_parity and lens:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        host0 = bufs[0][:args.config5_check].cpu().numpy()
+    res = {}
+    for avg in (2048, 8192, 65536):
+        sz = cfa.SizeParams(avg // 4, avg, avg * 8)
+        for name in ("ultra", "leap", "rabin", "seq"):
+            cls = {"rabin": cfa.RabinChunker, "ultra": cfa.UltraChunker, "leap": cfa.LeapChunker}.get(name)
+            ch = cls(sz, device=eng.local) if cls else cfa.SeqChunker(0, sz, device=eng.local)
+            cap = ch.batch_max_chunks(lens) if lens else 1
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=dev)
+            first = ch.chunk_batch_device(ptrs, lens, out.data_ptr(), cap) if lens else [0]
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if lens:
+                first = ch.chunk_batch_device(ptrs, lens, out.data_ptr(), cap)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            if world > 1:
+                dist.barrier()
+                el = sharding.max_over_ranks(el, red_dev)
+            line = {"sizes": [sz.min, sz.avg, sz.max], "GiBps": total / el / (1 << 30),
+                    "frac_of_hbm": total / el / 1e9 / HBM_PEAK_GBS / world,
+                    "chunks_total": sharding.sum_over_ranks(int(first[-1]), red_dev)}
+            if oracle is not None:
+                ref = oracle.cdc(name, host0, sz.min, sz.avg, sz.max)[:-1]
+                got = out[:len(ref)].cpu().numpy().view(np.uint64) if len(ref) else np.zeros((0, 2), np.uint64)
+                line["parity_vs_oracle"] = bool(got.shape == ref.shape and (got == ref).all())
+            res[f"{name}_avg{avg // 1024}k"] = line
+            ch.close()
+            del out
+    del bufs
+    return {"workload": f"config5: 16 x 1 GiB synthetic streams split across {world} GPU(s)", "scaling": "strong",
+            "streams_per_gpu": len(lens), "bytes_per_gpu": sum(lens),
+            "frac_definition": "per-GPU bytes / max-over-ranks time / 8 TB/s",
+            "parity_definition": f"rank 0, stream 0, the chunks inside its first {args.config5_check} B" if oracle
+            is not None else None, "lines": res}
 
 
 # ---------------------------------------------------------------------------
@@ -759,6 +835,10 @@ def main(argv=None):
         c4 = config4_leg(args, eng, rank, world, red_dev)
         if rank == 0:
             extras["config4"] = c4
+    if not args.no_config5 and not args.stub and args.workload == "stream":
+        c5 = config5_leg(args, eng, rank, world, red_dev)
+        if rank == 0:
+            extras["config5"] = c5
 
     traffic, traffic_src = traffic_for_build(args.traffic_json, bytes_rank)
     if rank == 0:

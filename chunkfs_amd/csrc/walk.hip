@@ -1032,13 +1032,10 @@ __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const W
             else nx[x >> 2] |= nxt << (8 * (x & 3));
         }
 #pragma unroll
-        for (int x = 63; x >= 0; --x) {
+        for (int x = 63; x >= 0; --x) {  // branch-free: every lane reads one slot
             const uint32_t n = (nx[x >> 2] >> (8 * (x & 3))) & 0xFFu;
-            uint32_t v;
-            if (n == 255u) v = 64u + (uint32_t)x;
-            else if (n >= 64u) v = n - 64u;
-            else v = res[n];
-            res[x] = (uint8_t)v;
+            const uint32_t r = res[n < 64u ? n : 0u];
+            res[x] = (uint8_t)(n == 255u ? 64u + (uint32_t)x : n >= 64u ? n - 64u : r);
         }
         if (in) {
             const uint32_t *r32 = reinterpret_cast<const uint32_t *>(res);
@@ -1057,16 +1054,14 @@ __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const W
         const uint32_t j = lane & 7;
         uint16_t o8[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < 3; ++q) {  // branch-free: 8 reads, selects
             uint32_t x = 3 * j + q, v = 0xFFFF;
 #pragma unroll
             for (int t = 0; t < 8; ++t) {
                 const uint32_t u = grp[t * kJSlot + x];
-                if (u >= 64) {
-                    v = 512u + 64u * t + (u - 64u);
-                    break;
-                }
-                x = u;
+                const bool hit = v == 0xFFFF && u >= 64;
+                v = hit ? 512u + 64u * t + (u - 64u) : v;
+                x = v == 0xFFFF ? u : x;
             }
             o8[q] = (uint16_t)(v == 0xFFFF ? x : v);
         }
@@ -1759,6 +1754,67 @@ __global__ __launch_bounds__(256) void ubits_kernel(const StreamTable st, const 
     }
 }
 
+// LeapCDC's bitmap pass: 4 pieces (waves) per block sharing 8 replicas of
+// the window-hash table (16 KiB; the single-copy table spent 4x its LDS
+// cycles in bank conflicts, profiles/r03_walk/pmcw_r03af), lane per
+// 64-position word, each byte's table value looked up once per word (the 4
+// bytes before the word once), the next word's loads in flight.
+constexpr int kLeapReps = 8;
+
+__device__ __forceinline__ void leap_load(uint4 (&v)[5], const uint8_t *base, uint64_t len, uint64_t p0) {
+    v[0] = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[1 + k] = load16_guarded(base, p0 + 16 * k, len);
+}
+
+__global__ __launch_bounds__(256) void lbits_kernel(const StreamTable st, const WalkParams wp) {
+    __shared__ uint64_t lt[256 * kLeapReps];
+    for (int i = threadIdx.x; i < 256 * kLeapReps; i += 256) lt[i] = wp.tabs[512 + i / kLeapReps];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    Piece pc;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), pc)) return;
+    const uint64_t *tl = lt + (lane & (kLeapReps - 1));
+    const uint64_t len = st.lens[pc.si];
+    const uint8_t *base = st.ptrs[pc.si];
+    const uint32_t reps = (uint32_t)((1ull << wp.piece_log2) >> 12);
+    const uint32_t thr = wp.leap_thr;
+    uint4 nx[5];
+    leap_load(nx, base, len, pc.off + 64ull * lane);
+    for (uint32_t it = 0; it < reps; ++it) {
+        const uint64_t lidx = (uint64_t)it * 64 + lane;
+        const uint64_t p0 = pc.off + lidx * 64;
+        if (p0 >= len) return;
+        uint4 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = nx[k];
+        if (it + 1 < reps && p0 + 4096 < len) leap_load(nx, base, len, p0 + 4096);
+        uint64_t e[20];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[16 + j] = tl[byte_of(v[0], 12 + j) * kLeapReps];
+        uint32_t pr[2] = {0, 0}, se[2] = {0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) e[j] = e[16 + j];  // the 4 bytes before this 16
+#pragma unroll
+            for (int j = 0; j < 16; ++j) e[4 + j] = tl[byte_of(v[1 + q], j) * kLeapReps];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint64_t h = 0;
+#pragma unroll
+                for (int k = 0; k < (int)CDC_LEAP_WSIZE; ++k) h += rotl64(e[4 + j - k], 11 * k);
+                const int bit = 16 * (q & 1) + j;
+                pr[q >> 1] |= (uint32_t)((uint32_t)(h >> 32) < thr) << bit;
+                se[q >> 1] |= (uint32_t)((uint32_t)h < thr) << bit;
+            }
+        }
+        uint64_t *out = wp.bm + (pc.wbase + lidx) * 2;
+        out[0] = ((uint64_t)pr[1] << 32) | pr[0];
+        out[1] = ((uint64_t)se[1] << 32) | se[0];
+    }
+}
+
 // ---- link mode (Rabin, UltraCDC, LeapCDC) ---------------------------------------
 // Candidates: the positions where a chunk can start after a cut that is not a
 // max / end / LEST cut, whatever the previous chunk's start -- so every such
@@ -2016,6 +2072,8 @@ hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t 
     else if (wp.algo == 4 && wp.bits_fine && wp.piece_log2 >= 12)
         ubits_kernel<<<(unsigned)((pieces + 3) / 4), 256, 0, s>>>(st, wp);
     else if (wp.algo == 4) bits_kernel<4><<<blocks, kWalkBlock, 0, s>>>(st, wp);
+    else if (wp.algo == 5 && wp.bits_fine && wp.piece_log2 >= 12)
+        lbits_kernel<<<(unsigned)((pieces + 3) / 4), 256, 0, s>>>(st, wp);
     else if (wp.algo == 5) bits_kernel<5><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 6) bits_kernel<6><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else return hipErrorInvalidValue;
