@@ -1647,16 +1647,23 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     }
 }
 
-// Rabin's bitmap pass with replicated tables: 4 segments (waves) per block
-// share 8 replicas of the mod / out tables (32 KiB of LDS; lane l reads
-// replica l & 7, entry e at (8 e + r) * 8, so at most 4 lanes of a 32-lane
-// bank group share a replica).  PMC of the single-copy tables showed 4x LDS
-// cycles in bank conflicts (profiles/r03_walk); 8 replicas with 4 waves per
-// block measured 610 us per GiB, 32 conflict-free replicas with 16 waves per
-// block (128 KiB, one block per CU) 687 us.  Lane l hashes 1/64 of its wave's segment from a
+// Rabin's bitmap pass with replicated tables: 8 pieces (waves) per block
+// share 16 replicas of the mod / out tables (64 KiB of LDS; lane l reads
+// replica l & 15, entry e at (16 e + r) * 8, so two lanes of a 32-lane bank
+// group share a replica).  PMC of the single-copy tables showed 4x LDS cycles
+// in bank conflicts (profiles/r03_walk); per GiB at 4/8/16 KiB, whole Rabin
+// call: 8 replicas x 4 waves 1293 GiB/s, 8 x 8 1294, 16 x 4 1051, 16 x 8
+// 1327, 32 x 16 (conflict-free, one block per CU) 1165
+// (profiles/r03_walk/r03ah_rabin_bits_variants.txt).  Lane l hashes 1/64 of its wave's segment from a
 // 48-byte warm-up (as bits_kernel<2>), the digest as two dwords.
-constexpr int kRabinReps = 8;
-constexpr int kRabinWaves = 4;  // segments per block (32 KiB of tables shared by 4 waves)
+#ifndef CDC_RABIN_REPS  // (experiment builds, tools/build_variants.py)
+#define CDC_RABIN_REPS 16
+#endif
+#ifndef CDC_RABIN_WAVES
+#define CDC_RABIN_WAVES 8
+#endif
+constexpr int kRabinReps = CDC_RABIN_REPS;
+constexpr int kRabinWaves = CDC_RABIN_WAVES;  // pieces per block (64 KiB of tables shared by 8 waves)
 
 __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTable st, const WalkParams wp) {
     __shared__ uint64_t rt[2 * 256 * kRabinReps];  // [table][entry][replica]: mod, out
