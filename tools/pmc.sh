@@ -2,7 +2,7 @@
 # PMC passes on the scan kernel (separate rocprofv3 runs, counters only, as
 # MI355X_MICROARCH.md prescribes).  Usage: tools/pmc.sh TAG [kernel-regex]
 TAG=${1:-r02}
-KRE=${2:-scan_kernel}
+KRE=${2:-p3::.*scan_kernel}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -25,7 +25,8 @@ def main():
     workload = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 30
     vals, name = [], None
     for r in csv.DictReader(open(src)):
-        if r["Counter_Name"] == "FETCH_SIZE" and "scan_kernel" in r["Kernel_Name"]:
+        # FastCDC's scan (cdc::p3::scan_kernel), not the walk engine's prefix scan
+        if r["Counter_Name"] == "FETCH_SIZE" and "p3::" in r["Kernel_Name"] and "scan_kernel" in r["Kernel_Name"]:
             vals.append(float(r["Counter_Value"]))
             name = r["Kernel_Name"]
     if not vals:
