@@ -804,6 +804,8 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     const bool jt = algo_ == CDC_ALGO_LEAP && wp_.wave;
     const size_t oJT = take(jt ? S * (size_t)wp_.seg_words * 24 : 0);  // LeapCDC word tables
     const size_t oJ8 = take(jt ? S * (size_t)wp_.seg_words * 6 : 0);   // and 512-position block tables
+    const bool rsum = algo_ == CDC_ALGO_ULTRA && wp_.wave;
+    const size_t oRS = take(rsum ? S * (size_t)wp_.seg_words / 8 : 0);  // UltraCDC repeat-word summary
     const size_t cc = wp_.links ? wp_.ccap : 0;                          // link mode
     const size_t oCN = take(S * 4), oCP = take(S * cc * 4), oLN = take(S * cc * 8), oLI = take(S * cc * 4);
     const size_t vc = wp_.links ? S * 8 : 0;
@@ -832,6 +834,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wp_.bm = wp_.nbm ? reinterpret_cast<uint64_t *>(b + oBM) : nullptr;
     wp_.jt = jt ? reinterpret_cast<uint8_t *>(b + oJT) : nullptr;
     wp_.jt8 = jt ? reinterpret_cast<uint16_t *>(b + oJ8) : nullptr;
+    wp_.rsum = rsum ? reinterpret_cast<uint64_t *>(b + oRS) : nullptr;
     wp_.ccnt = reinterpret_cast<uint32_t *>(b + oCN);
     wp_.cpos = reinterpret_cast<uint32_t *>(b + oCP);
     wp_.lnext = reinterpret_cast<uint64_t *>(b + oLN);

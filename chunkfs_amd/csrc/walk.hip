@@ -861,6 +861,77 @@ __device__ uint64_t wcut_ultra(const WBm &B, uint64_t s, uint64_t n, const WalkP
     return end;
 }
 
+// UltraCDC inside a run of 8-byte repeats.  When the LEST blocks at s + min,
+// s + min + 8, ... of a chunk starting at s are all repeats and the chunk can
+// reach s + Lr (Lr = min + 8 LEST: n >= Lr and max >= Lr), wcut_ultra's run
+// reaches LEST at its last block and the chunk is exactly Lr long, whatever
+// the hash bits say.  ultra_run returns k: the chain from c takes k such
+// chunks in a row (starts c + j Lr, j < k, all < lim), from the first
+// position >= c + min whose repeat bit is 0, found 4096 positions per wave
+// step in the repeat bitmap, then 256 KiB per step in the summary (rsum).
+constexpr uint64_t kUltraRun = (uint64_t)CDC_ULTRA_LEST * 8;
+
+__device__ uint64_t rep_first_zero(const WBm &B, const uint64_t *rs, uint64_t a, uint64_t need, uint32_t lane) {
+    const uint64_t ka = a >> 6;
+    {
+        const uint64_t k = ka + lane;
+        uint64_t w = B.word(3, 2, k);
+        if (k == ka) w |= (1ull << (a & 63)) - 1;  // positions before a count as repeats
+        const uint64_t m = __ballot(w != ~0ull && k * 64 < need);
+        if (m) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(m);
+            return min(need, (ka + f) * 64 + (uint64_t)__builtin_ctzll(~rdlane64(w, f)));
+        }
+    }
+    const uint64_t nsk = (B.nk + 63) >> 6;
+    for (uint64_t K = ka + 64; K * 64 < need; K = ((K >> 6) + 64) << 6) {
+        const uint64_t k0 = K >> 6, sk = k0 + lane;
+        uint64_t sw = 0;
+        if (sk < nsk) {
+            sw = rs[sk];
+            if (sk * 64 + 64 > B.nk) sw &= (1ull << (B.nk - sk * 64)) - 1;  // words past the stream end: 0
+        }
+        if (sk == k0) sw |= (1ull << (K & 63)) - 1;
+        const uint64_t m = __ballot(sw != ~0ull && sk * 4096 < need);
+        if (m) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(m);
+            const uint64_t kz = (k0 + f) * 64 + (uint64_t)__builtin_ctzll(~rdlane64(sw, f));
+            const uint64_t z = ~B.word(3, 2, kz);
+            return min(need, kz * 64 + (z ? (uint64_t)__builtin_ctzll(z) : 0));
+        }
+    }
+    return need;
+}
+
+__device__ uint64_t ultra_run(const WBm &B, const uint64_t *rs, uint64_t c, uint64_t len, uint64_t lim,
+                              const WalkParams &wp, uint32_t lane) {
+    const uint64_t Lr = wp.min + kUltraRun;
+    if (wp.max < Lr || c >= lim || len - c < Lr) return 0;
+    const uint64_t kmax = min((len - c) / Lr, (lim - c + Lr - 1) / Lr);
+    const uint64_t a = c + wp.min, tail = kUltraRun - 8;  // last block of a chunk: start + min + tail
+    const uint64_t b = rep_first_zero(B, rs, a, a + (kmax - 1) * Lr + tail + 1, lane);
+    return b > a + tail ? min(kmax, (b - a - tail + Lr - 1) / Lr) : 0;
+}
+
+// After a chunk of exactly min + 8 LEST (the trigger: a LEST cut, or rarely a
+// hash hit at that offset), take the repeat run's chunks from c at once: the
+// starts c + j Lr (j < k) go to list[cnt + j] (lanes in parallel).
+template <int kAlgo>
+__device__ __forceinline__ void take_run(const WBm &B, const uint64_t *rs, uint64_t d, uint64_t &c, uint64_t len,
+                                         uint64_t lim, const WalkParams &wp, uint32_t lane, uint64_t *list,
+                                         uint32_t &cnt) {
+    if constexpr (kAlgo == 4) {
+        const uint64_t Lr = wp.min + kUltraRun;
+        if (d != Lr || !rs || c >= lim) return;
+        const uint64_t k = ultra_run(B, rs, c, len, lim, wp, lane);
+        if (list)
+            for (uint64_t j = lane; j < k; j += 64)
+                if (cnt + j < wp.cap) list[cnt + j] = c + j * Lr;
+        cnt += (uint32_t)k;
+        c += k * Lr;
+    }
+}
+
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
     const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, o), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), o);
     return ((uint64_t)hi << 32) | lo;
@@ -1180,11 +1251,17 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
+    const uint64_t *rs = kAlgo == 4 && wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 : nullptr;
     uint64_t c = 0;
     if (off != 0) {  // warm-up start as walk_kernel (max-length grid)
         c = off > wp.warm ? off - wp.warm : 0;
         c = c / wp.max * wp.max;
-        while (c < off) c += wcut<kAlgo>(B, c, len - c, wp, lane);
+        uint32_t skip = 0;
+        while (c < off) {
+            const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
+            c += d;
+            take_run<kAlgo>(B, rs, d, c, len, off, wp, lane, nullptr, skip);
+        }
     }
     if (lane == 0) ws.E[g] = c;
     uint32_t cnt = 0;
@@ -1192,7 +1269,9 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
     while (c < seg_end) {
         if (lane == 0 && cnt < wp.cap) list[cnt] = c;
         ++cnt;
-        c += wcut<kAlgo>(B, c, len - c, wp, lane);
+        const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
+        c += d;
+        take_run<kAlgo>(B, rs, d, c, len, seg_end, wp, lane, list, cnt);
     }
     if (lane == 0) {
         ws.X[g] = c;
@@ -1205,8 +1284,8 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
 // from x until the new chain meets the old one (<= kNew new starts, kept in
 // the wave's LDS slots), else a full walk.  xo = the segment's exit after it.
 template <int kAlgo>
-__device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, const WBm &B, const WalkParams &wp,
-                        const WalkState &ws, uint64_t *nb, uint32_t lane, uint64_t &xo) {
+__device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, const WBm &B, const uint64_t *rs,
+                        const WalkParams &wp, const WalkState &ws, uint64_t *nb, uint32_t lane, uint64_t &xo) {
     uint64_t *list = ws.list + g * wp.cap;
     const uint32_t n_old = ws.N[g];
     const uint32_t lim = min(n_old, wp.cap);
@@ -1233,9 +1312,16 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
         }
         if (lane == 0) nb[m] = c;
         ++m;
-        c += wcut<kAlgo>(B, c, len - c, wp, lane);
+        const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
+        c += d;
+        if constexpr (kAlgo == 4) {  // a repeat run: chains keep their phase, walk it whole
+            if (d == wp.min + kUltraRun && rs && c < seg_end && ultra_run(B, rs, c, len, seg_end, wp, lane) >= 2) {
+                m = kNew + 1;
+                break;
+            }
+        }
     }
-    if (c >= seg_end) {  // the whole segment in <= kNew starts, no meeting point
+    if (c >= seg_end && m <= kNew) {  // the whole segment in <= kNew starts, no meeting point
         if (lane == 0) {
             for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
             ws.E[g] = x;
@@ -1251,7 +1337,9 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
     while (c < seg_end) {
         if (lane == 0 && cnt < wp.cap) list[cnt] = c;
         ++cnt;
-        c += wcut<kAlgo>(B, c, len - c, wp, lane);
+        const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
+        c += d;
+        take_run<kAlgo>(B, rs, d, c, len, seg_end, wp, lane, list, cnt);
     }
     if (lane == 0) {
         ws.E[g] = x;
@@ -1287,12 +1375,13 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
+    const uint64_t *rs = kAlgo == 4 && wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 : nullptr;
     uint64_t gg = g;
     for (uint32_t k = 0;; ++k) {
         const uint64_t seg_end = min(off + span, len);
         if (lane == 0) atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
         uint64_t xo;
-        if (!wrewalk<kAlgo>(x, gg, seg_end, len, B, wp, ws, nb, lane, xo)) break;
+        if (!wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, nb, lane, xo)) break;
         if (seg_end >= len) break;  // the stream's last segment: no successor
         if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
             if (lane == 0) {
@@ -1305,6 +1394,39 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
         ++gg;
         off += span;
     }
+}
+
+// The in-order pass inside a repeat run: the chain from x (segment g's
+// entry) takes k LEST chunks; every segment that ends at or before the run's
+// last start + Lr gets its list, entry, count and exit written directly
+// (lanes over chunks, then over segments).  Returns the first segment the
+// run does not cover whole (g: none), xe = its entry.
+__device__ uint64_t serial_run(const StreamTable &st, const WalkParams &wp, const WalkState &ws, const WBm &B,
+                               const uint64_t *rs, uint64_t g0, uint64_t g1, uint64_t g, uint64_t x, uint64_t len,
+                               uint32_t lane, uint64_t &xe) {
+    const uint64_t Lr = wp.min + kUltraRun;
+    const uint64_t k = ultra_run(B, rs, x, len, len, wp, lane);
+    const uint64_t ce = x + k * Lr;
+    const uint32_t sl = st.span_log2;
+    const uint64_t ie = min(ce >> sl, g1 - g0), i0 = g - g0;
+    if (k < 2 || ie <= i0) return g;
+    const uint64_t send = min(ie << sl, len);  // the covered segments end here
+    const uint64_t jtot = send > x ? (send - x + Lr - 1) / Lr : 0;  // run starts inside them
+    for (uint64_t j = lane; j < jtot; j += 64) {
+        const uint64_t p = x + j * Lr, i = p >> sl, o = i << sl;
+        const uint64_t jl = o > x ? (o - x + Lr - 1) / Lr : 0;
+        if (j - jl < wp.cap) ws.list[(g0 + i) * wp.cap + (j - jl)] = p;
+    }
+    for (uint64_t i = i0 + lane; i < ie; i += 64) {
+        const uint64_t o = i << sl, e = min(o + (1ull << sl), len);
+        const uint64_t jl = o > x ? (o - x + Lr - 1) / Lr : 0, jh = e > x ? (e - x + Lr - 1) / Lr : 0;
+        ws.E[g0 + i] = x + jl * Lr;
+        ws.X[g0 + i] = x + jh * Lr;
+        ws.N[g0 + i] = (uint32_t)(jh - jl);
+        if (jh - jl > wp.cap) atomicAdd(&ws.flags[1], 1ull);
+    }
+    xe = x + jtot * Lr;
+    return g0 + ie;
 }
 
 // serial_kernel with a wave per stream (wave-cooperative re-walks).  The exit
@@ -1325,16 +1447,27 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + g0 * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
+    const uint64_t *rs = kAlgo == 4 && wp.rsum ? wp.rsum + g0 * (uint64_t)wp.seg_words / 64 : nullptr;
     uint64_t xprev = 0;
     bool have = false;
     for (uint64_t g = max(g0 + 1, (uint64_t)ws.flags[2]); g < g1; ++g) {
         const uint64_t x = have ? xprev : ws.X[g - 1];
         have = false;
         if (ws.E[g] == x) continue;
+        if constexpr (kAlgo == 4) {
+            uint64_t xe;
+            const uint64_t ge = rs ? serial_run(st, wp, ws, B, rs, g0, g1, g, x, len, lane, xe) : g;
+            if (ge > g) {  // segments g .. ge-1 lie wholly inside one repeat run
+                xprev = xe;
+                have = true;
+                g = ge - 1;
+                continue;
+            }
+        }
         const uint64_t off = (g - g0) << st.span_log2;
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
         uint64_t xo;
-        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, wp, ws, nb, lane, xo);
+        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, rs, wp, ws, nb, lane, xo);
         xprev = xo;
         have = true;
     }
@@ -1395,7 +1528,7 @@ __device__ __forceinline__ void for_chunks(const uint8_t *base, uint64_t len, ui
 // UltraCDC predicate bits of one 64-position word from its bytes w[4..19]
 // (w[0..3] = the 16 bytes before, w[20..23] = the 16 after): bitmaps 0
 // (dist & MASK_S == 0), 1 (dist & MASK_L == 0), 2 (8-byte repeat).
-__device__ __forceinline__ void ultra_word(const uint32_t (&w)[24], uint64_t *out) {
+__device__ __forceinline__ uint64_t ultra_word(const uint32_t (&w)[24], uint64_t *out) {
     // equality bits E(i) = (b[i] == b[i-8]) for i = p0 .. p0+71 (first:
     // w is dead after the popcounts, which keeps the kernel's VGPRs low)
     uint32_t e[3] = {0, 0, 0};
@@ -1439,6 +1572,7 @@ __device__ __forceinline__ void ultra_word(const uint32_t (&w)[24], uint64_t *ou
     out[0] = ~(((uint64_t)hs1 << 32) | hs0);
     out[1] = ~(((uint64_t)hl1 << 32) | hl0);
     out[2] = (uint64_t)a8;
+    return (uint64_t)a8;
 }
 
 template <int kAlgo>
@@ -1757,7 +1891,10 @@ __global__ __launch_bounds__(256) void ubits_kernel(const StreamTable st, const 
             w[4 * k] = nx[k].x; w[4 * k + 1] = nx[k].y; w[4 * k + 2] = nx[k].z; w[4 * k + 3] = nx[k].w;
         }
         if (it + 1 < reps && p0 + 4096 < len) ultra_load(nx, base, len, p0 + 4096);
-        ultra_word(w, wp.bm + (pc.wbase + lidx) * 3);
+        const uint64_t rep = ultra_word(w, wp.bm + (pc.wbase + lidx) * 3);
+        // the 64 words' all-repeat bits (lanes past the stream end: 0)
+        const uint64_t full = __ballot(rep == ~0ull);
+        if (wp.rsum && lane == 0) wp.rsum[(pc.wbase >> 6) + it] = full;
     }
 }
 
@@ -2002,7 +2139,7 @@ __global__ __launch_bounds__(kScanBlock) void sum_kernel(const StreamTable st, c
 }
 
 // One block: exclusive prefix of the nb block sums in place; bsum[nb] = total.
-__global__ __launch_bounds__(kScanBlock) void scan_kernel(const WalkState ws, uint64_t nb) {
+__global__ __launch_bounds__(kScanBlock) void prefix_kernel(const WalkState ws, uint64_t nb) {
     __shared__ uint64_t sh[kScanBlock];
     uint64_t carry = 0;
     for (uint64_t b0 = 0; b0 < nb; b0 += kScanBlock) {
@@ -2143,7 +2280,7 @@ hipError_t launch_emit(const StreamTable &st, const WalkParams &wp, const WalkSt
     const uint64_t nb = (st.total_spans + kScanBlock - 1) / kScanBlock;
     if (nb) {
         sum_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, ws);
-        scan_kernel<<<1, kScanBlock, 0, s>>>(ws, nb);
+        prefix_kernel<<<1, kScanBlock, 0, s>>>(ws, nb);
         emit_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, wp, ws, reinterpret_cast<cdc_chunk_pod *>(d_out),
                                                         out_cap);
     }

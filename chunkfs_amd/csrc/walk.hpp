@@ -70,6 +70,12 @@ struct WalkParams {
     // block, jt8[b * 24 + e] (u16): < 24 = entry into block b + 1, >= 512 =
     // accepted at 512 b + (v - 512).
     uint16_t *jt8;
+    // UltraCDC wave walks: one bit per repeat-bitmap word, bit k & 63 of
+    // rsum[k >> 6] (k = segment g's word index + g * seg_words): all 64
+    // positions of the word are 8-byte repeats.  A chain inside a long run
+    // of repeats (zero-filled or 8-byte-periodic regions) takes its LEST
+    // chunks many at a time (ultra_run) instead of one wcut per chunk.
+    uint64_t *rsum;
 };
 
 constexpr uint32_t kNoCand = 0xFFFFFFFFu;

@@ -272,3 +272,61 @@ def test_fixup_schedules_exact(algo, walk, ahead, monkeypatch):
     data = make_input("periodic", 600000, 61)
     assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} periodic walk={walk} ahead={ahead}")
     ch.close()
+
+
+def repeat_run_stream(n, seed):
+    """Random bytes with long 8-byte-repeat regions at unaligned offsets: zero
+    runs (one of them broken by single bytes), a constant byte, an 8-byte
+    period -- where UltraCDC chains keep their phase (LEST chunks) and the
+    walks take them many at a time (walk.hip ultra_run / serial_run)."""
+    d = oracle.splitmix64_bytes(n, seed)
+    rng = np.random.default_rng(seed)
+    pos = 12345
+    while pos < n - 64:
+        ln = int(rng.integers(1, 6 << 20))
+        kind = int(rng.integers(0, 4))
+        e = min(n, pos + ln)
+        if kind == 0:
+            d[pos:e] = 0
+        elif kind == 1:
+            d[pos:e] = 0x41
+        elif kind == 2:
+            d[pos:e] = np.resize(np.arange(8, dtype=np.uint8) * 37 + 1, e - pos)
+        else:
+            d[pos:e] = 0
+            d[pos:e:int(rng.integers(20000, 300000))] = 7
+        pos = e + int(rng.integers(1000, 2 << 20))
+    return d
+
+
+@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (512, 2048, 16384), (2048, 8192, 65536),
+                                   (16384, 65536, 524288)])
+def test_ultra_repeat_runs_exact(sizes):
+    """UltraCDC over long repeat runs in a 3-stream device batch (40 MiB, 24 MiB
+    of zeros, 7 MiB + 1): bit-exact vs the oracle."""
+    import torch
+    lens = [40 << 20, 24 << 20, (7 << 20) + 1]
+    hosts = [repeat_run_stream(lens[0], 31), np.zeros(lens[1], dtype=np.uint8), repeat_run_stream(lens[2], 32)]
+    devs = [torch.from_numpy(h).to("cuda:0") for h in hosts]
+    ch = chunker("ultra", sizes)
+    cap = ch.batch_max_chunks(lens)
+    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    first = ch.chunk_batch_device([d.data_ptr() for d in devs], lens, out.data_ptr(), cap)
+    got = out[:first[-1]].cpu().numpy().astype(np.uint64)
+    for i, h in enumerate(hosts):
+        assert_same(got[first[i]:first[i + 1]], oracle.cdc("ultra", h, *sizes), f"ultra {sizes} stream {i}")
+
+
+@pytest.mark.parametrize("walk,ahead", [("13,2", "16,1"), ("17,1", "0,64")])
+def test_ultra_repeat_runs_serial_pass(walk, ahead, monkeypatch):
+    """The in-order pass over repeat runs (segment lists written per run,
+    serial_run): schedules that leave most segments to it."""
+    import chunkfs_amd as c
+    monkeypatch.setenv("CHUNKFS_AMD_WALK", walk)
+    monkeypatch.setenv("CHUNKFS_AMD_AHEAD", ahead)
+    sizes = (4096, 8192, 16384)
+    ch = c.UltraChunker(c.SizeParams(*sizes))
+    for data in (np.zeros((16 << 20) + 77, dtype=np.uint8), repeat_run_stream(24 << 20, 33)):
+        assert_same(ch.chunk_array(data), oracle.cdc("ultra", data, *sizes), f"ultra serial {walk} {ahead}")
+    ch.close()

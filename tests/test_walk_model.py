@@ -301,3 +301,54 @@ def test_ultra_block_windows_model(data):
         pos += cut
     ref = oracle.cdc("ultra", d, mn, avg, mx)
     assert np.array_equal(np.array(got, dtype=np.uint64).reshape(-1, 2), ref)
+
+
+def ultra_run(rep, c, n, lim, mn, mx, LEST):
+    """walk.hip ultra_run: LEST chunks the chain takes at once from c inside a
+    run of 8-byte repeats (starts < lim), from the first non-repeat position
+    at or after c + min."""
+    Lr = mn + 8 * LEST
+    if mx < Lr or c >= lim or n - c < Lr:
+        return 0
+    kmax = min((n - c) // Lr, (lim - c + Lr - 1) // Lr)
+    a, tail = c + mn, 8 * LEST - 8
+    need = a + (kmax - 1) * Lr + tail + 1
+    z = np.nonzero(~rep[a:need])[0]
+    b = a + int(z[0]) if z.size else need
+    return min(kmax, (b - a - tail + Lr - 1) // Lr) if b > a + tail else 0
+
+
+def repeat_regions(n, seed):
+    d = oracle.splitmix64_bytes(n, seed)
+    d[10007:10007 + 300000] = 0                                   # zeros, unaligned
+    d[400001:400001 + 123457] = 0x41                              # a constant byte
+    d[600003:600003 + 250000] = np.resize(np.arange(8, dtype=np.uint8) * 37, 250000)  # 8-byte period
+    d[900000:900000 + 70000] = 0
+    d[900000 + 33333] = 1                                         # one break inside a zero run
+    return d
+
+
+@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (512, 2048, 16384), (2048, 8192, 65536)])
+def test_ultra_repeat_runs_model(sizes):
+    """Chains that take a repeat run's LEST chunks many at a time (ultra_run
+    after a chunk of exactly min + 8 LEST) cut exactly where the oracle does."""
+    mn, avg, mx = sizes
+    LEST = P["CDC_ULTRA_LEST"]
+    Lr = mn + 8 * LEST
+    n = (1 << 20) + 4321
+    d = repeat_regions(n, 9)
+    hs, hl, rep = ultra_bitmaps(d)
+    got, pos, jumped = [], 0, 0
+    while pos < n:
+        cut = wcut_ultra(hs, hl, rep, pos, n - pos, mn, avg, mx, LEST)
+        got.append((pos, cut))
+        pos += cut
+        if cut == Lr:
+            k = ultra_run(rep, pos, n, n, mn, mx, LEST)
+            got += [(pos + j * Lr, Lr) for j in range(k)]
+            pos += k * Lr
+            jumped += k
+    ref = oracle.cdc("ultra", d, mn, avg, mx)
+    assert np.array_equal(np.array(got, dtype=np.uint64).reshape(-1, 2), ref)
+    if mx >= Lr:
+        assert jumped > 0
