@@ -510,7 +510,8 @@ def algo_lines(args, eng, w, steps):
 
 def lowentropy_walk_lines(args, eng, nbytes=256 << 20):
     """Rabin / UltraCDC / LeapCDC / SeqCDC on low-entropy device streams of
-    `nbytes` (zeros; a 61-byte period), bench sizes: chains from different
+    `nbytes` (zeros; a 61-byte period; random bytes with 1-32 MiB zero-filled
+    regions at unaligned offsets), bench sizes: chains from different
     starts never merge on such data, so these lines time the fix-up rounds
     and the in-order pass (one wave per stream) that the splitmix64 lines
     never reach.  Device GiB/s, the re-walk statistics and bit-exactness vs
@@ -522,8 +523,18 @@ def lowentropy_walk_lines(args, eng, nbytes=256 << 20):
     import oracle
     n = nbytes
     period = torch.from_numpy(oracle.splitmix64_bytes(61, 7)).to(eng.dev)
+    # a sparse-image shape: random bytes with zero-filled regions of 1-32 MiB at
+    # unaligned offsets (chains enter each region at an arbitrary phase)
+    runs = torch.from_numpy(oracle.splitmix64_bytes(n, 17)).to(eng.dev)
+    rng = np.random.default_rng(17)
+    pos = int(rng.integers(1, 1 << 20))
+    while pos < n:
+        ln = int(rng.integers(1 << 20, 32 << 20))
+        runs[pos:pos + ln] = 0
+        pos += ln + int(rng.integers(1 << 16, 8 << 20))
     inputs = {"zeros": torch.zeros(n, dtype=torch.uint8, device=eng.dev),
-              "periodic61": period.repeat(-(-n // 61))[:n].contiguous()}
+              "periodic61": period.repeat(-(-n // 61))[:n].contiguous(),
+              "zero_runs": runs}
     sizes = cfa.SizeParams(args.min, args.avg, args.max)
     res = {}
     for inp, buf in inputs.items():

@@ -804,8 +804,9 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     const bool jt = algo_ == CDC_ALGO_LEAP && wp_.wave;
     const size_t oJT = take(jt ? S * (size_t)wp_.seg_words * 24 : 0);  // LeapCDC word tables
     const size_t oJ8 = take(jt ? S * (size_t)wp_.seg_words * 6 : 0);   // and 512-position block tables
-    const bool rsum = algo_ == CDC_ALGO_ULTRA && wp_.wave;
-    const size_t oRS = take(rsum ? S * (size_t)wp_.seg_words / 8 : 0);  // UltraCDC repeat-word summary
+    bool rsum = walk::bits_write_summary(wp_);  // quiet runs (CHUNKFS_AMD_QUIET=0: off, A/B)
+    if (const char *q = std::getenv("CHUNKFS_AMD_QUIET")) rsum = rsum && std::atoi(q) != 0;
+    const size_t oRS = take(rsum ? S * (size_t)wp_.seg_words / 8 * (algo_ == CDC_ALGO_RABIN ? 2 : 1) : 0);  // quiet-run summary
     const size_t cc = wp_.links ? wp_.ccap : 0;                          // link mode
     const size_t oCN = take(S * 4), oCP = take(S * cc * 4), oLN = take(S * cc * 8), oLI = take(S * cc * 4);
     const size_t vc = wp_.links ? S * 8 : 0;

@@ -861,75 +861,161 @@ __device__ uint64_t wcut_ultra(const WBm &B, uint64_t s, uint64_t n, const WalkP
     return end;
 }
 
-// UltraCDC inside a run of 8-byte repeats.  When the LEST blocks at s + min,
-// s + min + 8, ... of a chunk starting at s are all repeats and the chunk can
-// reach s + Lr (Lr = min + 8 LEST: n >= Lr and max >= Lr), wcut_ultra's run
-// reaches LEST at its last block and the chunk is exactly Lr long, whatever
-// the hash bits say.  ultra_run returns k: the chain from c takes k such
-// chunks in a row (starts c + j Lr, j < k, all < lim), from the first
-// position >= c + min whose repeat bit is 0, found 4096 positions per wave
-// step in the repeat bitmap, then 256 KiB per step in the summary (rsum).
-constexpr uint64_t kUltraRun = (uint64_t)CDC_ULTRA_LEST * 8;
+// Quiet runs.  Inside long zero-filled or constant regions every chunk of a
+// rule has one fixed length L, so chains keep the phase they enter with and
+// never merge; there the walks take the region's chunks many at a time.  Per
+// rule (and kind), a chunk starting at s has length exactly L when every
+// position of [s + lo, s + hi] is "quiet" and len - s >= L:
+//   Rabin 0, Seq  L = max:          no hit / no in-direction pair in
+//                                   [s+min-1, s+max-1] (no cut before max);
+//   Rabin 1       L = min:          a hit at s+min-1 (zeros: the digest of a
+//                                   zero window is 0, a hit everywhere);
+//   UltraCDC      L = min + 8 LEST: every block from s+min an 8-byte repeat
+//                                   (the run reaches LEST whatever the hashes);
+//   LeapCDC       L = min:          primary and secondary windows all eligible
+//                                   in [s+min-24, s+min-1] (accepted at once).
+// quiet_run finds the first loud position at or after c + lo (4096 positions
+// per wave step in the bitmaps, then 2 MiB per step in the per-word summary
+// wp.rsum, written by the bitmap pass: kinds interleaved per summary word)
+// and returns k: the chain from c takes k chunks of length L in a row, the k
+// starts all < lim.
+struct QuietRule {
+    uint64_t L, lo, hi;
+    bool ok;
+};
 
-__device__ uint64_t rep_first_zero(const WBm &B, const uint64_t *rs, uint64_t a, uint64_t need, uint32_t lane) {
+template <int kAlgo>
+constexpr int kQuietKinds = kAlgo == 2 ? 2 : 1;
+
+template <int kAlgo, int kKind>
+__device__ __forceinline__ QuietRule quiet_rule(const WalkParams &wp) {
+    if constexpr (kAlgo == 4) {
+        const uint64_t L = wp.min + 8ull * CDC_ULTRA_LEST;
+        return {L, wp.min, L - 8, wp.max >= L};
+    } else if constexpr (kAlgo == 5) {
+        return {wp.min, wp.min - CDC_LEAP_WINDOWS, wp.min - 1, wp.min >= CDC_LEAP_WINDOWS};
+    } else if constexpr (kKind == 1) {
+        return {wp.min, wp.min - 1, wp.min - 1, wp.min >= 1 && wp.min < wp.max};
+    } else {
+        return {wp.max, wp.min - 1, wp.max - 1, wp.min >= 1};
+    }
+}
+
+// Loud (non-quiet) positions of word k, bit j = position 64 k + j.
+template <int kAlgo, int kKind>
+__device__ __forceinline__ uint64_t loud_word(const WBm &B, uint64_t k) {
+    if constexpr (kAlgo == 4) return ~B.word(3, 2, k);
+    else if constexpr (kAlgo == 5) return ~(B.word(2, 0, k) & B.word(2, 1, k));
+    else if constexpr (kKind == 1) return ~B.word(1, 0, k);
+    else return B.word(1, 0, k);
+}
+
+// First loud position in [a, need), else need.  Summary bits of words at or
+// past the stream end read loud (their summary words may be stale).
+template <int kAlgo, int kKind>
+__device__ uint64_t first_loud(const WBm &B, const uint64_t *rs, uint64_t a, uint64_t need, uint32_t lane) {
     const uint64_t ka = a >> 6;
     {
         const uint64_t k = ka + lane;
-        uint64_t w = B.word(3, 2, k);
-        if (k == ka) w |= (1ull << (a & 63)) - 1;  // positions before a count as repeats
-        const uint64_t m = __ballot(w != ~0ull && k * 64 < need);
+        uint64_t w = loud_word<kAlgo, kKind>(B, k);
+        if (k == ka) w &= ~0ull << (a & 63);  // positions before a do not count
+        const uint64_t m = __ballot(w != 0 && k * 64 < need);
         if (m) {
             const uint32_t f = (uint32_t)__builtin_ctzll(m);
-            return min(need, (ka + f) * 64 + (uint64_t)__builtin_ctzll(~rdlane64(w, f)));
+            return min(need, (ka + f) * 64 + (uint64_t)__builtin_ctzll(rdlane64(w, f)));
         }
     }
+    // summary words from word K on: lane l reads words k0 + 8 l .. + 7
+    constexpr uint32_t kPer = 8;
     const uint64_t nsk = (B.nk + 63) >> 6;
-    for (uint64_t K = ka + 64; K * 64 < need; K = ((K >> 6) + 64) << 6) {
-        const uint64_t k0 = K >> 6, sk = k0 + lane;
-        uint64_t sw = 0;
-        if (sk < nsk) {
-            sw = rs[sk];
-            if (sk * 64 + 64 > B.nk) sw &= (1ull << (B.nk - sk * 64)) - 1;  // words past the stream end: 0
+    for (uint64_t K = ka + 64; K * 64 < need; K = ((K >> 6) + 64 * kPer) << 6) {
+        const uint64_t k0 = K >> 6;
+        uint32_t fi = kPer;
+        uint64_t fw = ~0ull;
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint64_t sk = k0 + kPer * lane + i;
+            uint64_t sw = 0;
+            if (sk < nsk) {
+                sw = rs[sk * kQuietKinds<kAlgo> + kKind];
+                if (sk * 64 + 64 > B.nk) sw &= (1ull << (B.nk - sk * 64)) - 1;
+            }
+            if (sk == k0) sw |= (1ull << (K & 63)) - 1;
+            if (sk * 4096 >= need) sw = ~0ull;
+            const bool hit = sw != ~0ull && fi == kPer;
+            fw = hit ? sw : fw;
+            fi = hit ? i : fi;
         }
-        if (sk == k0) sw |= (1ull << (K & 63)) - 1;
-        const uint64_t m = __ballot(sw != ~0ull && sk * 4096 < need);
+        const uint64_t m = __ballot(fi < kPer);
         if (m) {
             const uint32_t f = (uint32_t)__builtin_ctzll(m);
-            const uint64_t kz = (k0 + f) * 64 + (uint64_t)__builtin_ctzll(~rdlane64(sw, f));
-            const uint64_t z = ~B.word(3, 2, kz);
+            const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)fi, (int)f);
+            const uint64_t kz = (k0 + kPer * f + i) * 64 + (uint64_t)__builtin_ctzll(~rdlane64(fw, f));
+            const uint64_t z = loud_word<kAlgo, kKind>(B, kz);
             return min(need, kz * 64 + (z ? (uint64_t)__builtin_ctzll(z) : 0));
         }
     }
     return need;
 }
 
-__device__ uint64_t ultra_run(const WBm &B, const uint64_t *rs, uint64_t c, uint64_t len, uint64_t lim,
+template <int kAlgo, int kKind>
+__device__ uint64_t quiet_run(const WBm &B, const uint64_t *rs, uint64_t c, uint64_t len, uint64_t lim,
                               const WalkParams &wp, uint32_t lane) {
-    const uint64_t Lr = wp.min + kUltraRun;
-    if (wp.max < Lr || c >= lim || len - c < Lr) return 0;
-    const uint64_t kmax = min((len - c) / Lr, (lim - c + Lr - 1) / Lr);
-    const uint64_t a = c + wp.min, tail = kUltraRun - 8;  // last block of a chunk: start + min + tail
-    const uint64_t b = rep_first_zero(B, rs, a, a + (kmax - 1) * Lr + tail + 1, lane);
-    return b > a + tail ? min(kmax, (b - a - tail + Lr - 1) / Lr) : 0;
+    const QuietRule q = quiet_rule<kAlgo, kKind>(wp);
+    if (!q.ok || c >= lim || len - c < q.L) return 0;
+    const uint64_t kmax = min((len - c) / q.L, (lim - c + q.L - 1) / q.L);
+    const uint64_t a = c + q.lo, tail = q.hi - q.lo;
+    const uint64_t b = first_loud<kAlgo, kKind>(B, rs, a, a + (kmax - 1) * q.L + tail + 1, lane);
+    return b > a + tail ? min(kmax, (b - a - tail + q.L - 1) / q.L) : 0;
 }
 
-// After a chunk of exactly min + 8 LEST (the trigger: a LEST cut, or rarely a
-// hash hit at that offset), take the repeat run's chunks from c at once: the
-// starts c + j Lr (j < k) go to list[cnt + j] (lanes in parallel).
+// The kind a chunk of length d may start (-1: none).
 template <int kAlgo>
-__device__ __forceinline__ void take_run(const WBm &B, const uint64_t *rs, uint64_t d, uint64_t &c, uint64_t len,
-                                         uint64_t lim, const WalkParams &wp, uint32_t lane, uint64_t *list,
-                                         uint32_t &cnt) {
-    if constexpr (kAlgo == 4) {
-        const uint64_t Lr = wp.min + kUltraRun;
-        if (d != Lr || !rs || c >= lim) return;
-        const uint64_t k = ultra_run(B, rs, c, len, lim, wp, lane);
-        if (list)
-            for (uint64_t j = lane; j < k; j += 64)
-                if (cnt + j < wp.cap) list[cnt + j] = c + j * Lr;
-        cnt += (uint32_t)k;
-        c += k * Lr;
+__device__ __forceinline__ int quiet_kind(const WalkParams &wp, uint64_t d) {
+    if (d == quiet_rule<kAlgo, 0>(wp).L) return 0;
+    if constexpr (kQuietKinds<kAlgo> > 1)
+        if (d == quiet_rule<kAlgo, 1>(wp).L) return 1;
+    return -1;
+}
+
+template <int kAlgo>
+__device__ __forceinline__ uint64_t quiet_run_k(int kind, const WBm &B, const uint64_t *rs, uint64_t c, uint64_t len,
+                                                uint64_t lim, const WalkParams &wp, uint32_t lane, uint64_t &L) {
+    if constexpr (kQuietKinds<kAlgo> > 1) {
+        if (kind == 1) {
+            L = quiet_rule<kAlgo, 1>(wp).L;
+            return quiet_run<kAlgo, 1>(B, rs, c, len, lim, wp, lane);
+        }
     }
+    L = quiet_rule<kAlgo, 0>(wp).L;
+    return quiet_run<kAlgo, 0>(B, rs, c, len, lim, wp, lane);
+}
+
+// In a walk, after a chunk of one kind's length L (Rabin: two in a row, pk
+// = the previous chunk's kind; max-length chunks are common in its random
+// data, and its quiet search is the next hit's), take the quiet run's chunks
+// from c at once: the starts c + j L (j < k) go to list[cnt + j] (lanes in
+// parallel).
+template <int kAlgo>
+constexpr bool kQuietTwice = kAlgo == 2;
+
+template <int kAlgo>
+__device__ __forceinline__ void take_run(const WBm &B, const uint64_t *rs, uint64_t d, int &pk, uint64_t &c,
+                                         uint64_t len, uint64_t lim, const WalkParams &wp, uint32_t lane,
+                                         uint64_t *list, uint32_t &cnt) {
+    const int kind = quiet_kind<kAlgo>(wp, d);
+    if (kind < 0 || (kQuietTwice<kAlgo> && kind != pk) || !rs || c >= lim) {
+        pk = kind;
+        return;
+    }
+    uint64_t L;
+    const uint64_t k = quiet_run_k<kAlgo>(kind, B, rs, c, len, lim, wp, lane, L);
+    if (list)
+        for (uint64_t j = lane; j < k; j += 64)
+            if (cnt + j < wp.cap) list[cnt + j] = c + j * L;
+    cnt += (uint32_t)k;
+    c += k * L;
+    pk = k ? kind : -1;
 }
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
@@ -1251,8 +1337,9 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
-    const uint64_t *rs = kAlgo == 4 && wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 : nullptr;
+    const uint64_t *rs = wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t c = 0;
+    int pk = -1;
     if (off != 0) {  // warm-up start as walk_kernel (max-length grid)
         c = off > wp.warm ? off - wp.warm : 0;
         c = c / wp.max * wp.max;
@@ -1260,7 +1347,7 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
         while (c < off) {
             const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
             c += d;
-            take_run<kAlgo>(B, rs, d, c, len, off, wp, lane, nullptr, skip);
+            take_run<kAlgo>(B, rs, d, pk, c, len, off, wp, lane, nullptr, skip);
         }
     }
     if (lane == 0) ws.E[g] = c;
@@ -1271,7 +1358,7 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
         ++cnt;
         const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
         c += d;
-        take_run<kAlgo>(B, rs, d, c, len, seg_end, wp, lane, list, cnt);
+        take_run<kAlgo>(B, rs, d, pk, c, len, seg_end, wp, lane, list, cnt);
     }
     if (lane == 0) {
         ws.X[g] = c;
@@ -1292,6 +1379,7 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
     const uint64_t x_old = ws.X[g];
     uint64_t c = x;
     uint32_t m = 0, j = 0;
+    int pk = -1;
     while (c < seg_end && m < kNew) {
         while (j < lim && list[j] < c) ++j;
         if (j < lim && list[j] == c) {  // meets the old chain at old start j
@@ -1314,12 +1402,14 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
         ++m;
         const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
         c += d;
-        if constexpr (kAlgo == 4) {  // a repeat run: chains keep their phase, walk it whole
-            if (d == wp.min + kUltraRun && rs && c < seg_end && ultra_run(B, rs, c, len, seg_end, wp, lane) >= 2) {
-                m = kNew + 1;
-                break;
-            }
+        const int kind = quiet_kind<kAlgo>(wp, d);  // a quiet run: chains keep their phase, walk it whole
+        uint64_t L;
+        if (kind >= 0 && (!kQuietTwice<kAlgo> || kind == pk) && rs && c < seg_end &&
+            quiet_run_k<kAlgo>(kind, B, rs, c, len, seg_end, wp, lane, L) >= 2) {
+            m = kNew + 1;
+            break;
         }
+        pk = kind;
     }
     if (c >= seg_end && m <= kNew) {  // the whole segment in <= kNew starts, no meeting point
         if (lane == 0) {
@@ -1334,12 +1424,13 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
     // full walk from x
     c = x;
     uint32_t cnt = 0;
+    pk = -1;
     while (c < seg_end) {
         if (lane == 0 && cnt < wp.cap) list[cnt] = c;
         ++cnt;
         const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
         c += d;
-        take_run<kAlgo>(B, rs, d, c, len, seg_end, wp, lane, list, cnt);
+        take_run<kAlgo>(B, rs, d, pk, c, len, seg_end, wp, lane, list, cnt);
     }
     if (lane == 0) {
         ws.E[g] = x;
@@ -1375,7 +1466,7 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
-    const uint64_t *rs = kAlgo == 4 && wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 : nullptr;
+    const uint64_t *rs = wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t gg = g;
     for (uint32_t k = 0;; ++k) {
         const uint64_t seg_end = min(off + span, len);
@@ -1396,36 +1487,39 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     }
 }
 
-// The in-order pass inside a repeat run: the chain from x (segment g's
-// entry) takes k LEST chunks; every segment that ends at or before the run's
-// last start + Lr gets its list, entry, count and exit written directly
-// (lanes over chunks, then over segments).  Returns the first segment the
-// run does not cover whole (g: none), xe = its entry.
+// The in-order pass inside a quiet run: the chain from x (segment g's entry)
+// takes k chunks of length L; every segment that ends at or before the run's
+// covered part gets its list, entry, count and exit written directly (lanes
+// over chunks, then over segments).  Returns the first segment the run does
+// not cover whole (g: none), xe = its entry.
+template <int kAlgo>
 __device__ uint64_t serial_run(const StreamTable &st, const WalkParams &wp, const WalkState &ws, const WBm &B,
                                const uint64_t *rs, uint64_t g0, uint64_t g1, uint64_t g, uint64_t x, uint64_t len,
                                uint32_t lane, uint64_t &xe) {
-    const uint64_t Lr = wp.min + kUltraRun;
-    const uint64_t k = ultra_run(B, rs, x, len, len, wp, lane);
-    const uint64_t ce = x + k * Lr;
+    uint64_t L;
+    uint64_t k = quiet_run_k<kAlgo>(0, B, rs, x, len, len, wp, lane, L);
+    if constexpr (kQuietKinds<kAlgo> > 1)
+        if (k < 2) k = quiet_run_k<kAlgo>(1, B, rs, x, len, len, wp, lane, L);
+    const uint64_t ce = x + k * L;
     const uint32_t sl = st.span_log2;
     const uint64_t ie = min(ce >> sl, g1 - g0), i0 = g - g0;
     if (k < 2 || ie <= i0) return g;
     const uint64_t send = min(ie << sl, len);  // the covered segments end here
-    const uint64_t jtot = send > x ? (send - x + Lr - 1) / Lr : 0;  // run starts inside them
+    const uint64_t jtot = send > x ? (send - x + L - 1) / L : 0;  // run starts inside them
     for (uint64_t j = lane; j < jtot; j += 64) {
-        const uint64_t p = x + j * Lr, i = p >> sl, o = i << sl;
-        const uint64_t jl = o > x ? (o - x + Lr - 1) / Lr : 0;
+        const uint64_t p = x + j * L, i = p >> sl, o = i << sl;
+        const uint64_t jl = o > x ? (o - x + L - 1) / L : 0;
         if (j - jl < wp.cap) ws.list[(g0 + i) * wp.cap + (j - jl)] = p;
     }
     for (uint64_t i = i0 + lane; i < ie; i += 64) {
         const uint64_t o = i << sl, e = min(o + (1ull << sl), len);
-        const uint64_t jl = o > x ? (o - x + Lr - 1) / Lr : 0, jh = e > x ? (e - x + Lr - 1) / Lr : 0;
-        ws.E[g0 + i] = x + jl * Lr;
-        ws.X[g0 + i] = x + jh * Lr;
+        const uint64_t jl = o > x ? (o - x + L - 1) / L : 0, jh = e > x ? (e - x + L - 1) / L : 0;
+        ws.E[g0 + i] = x + jl * L;
+        ws.X[g0 + i] = x + jh * L;
         ws.N[g0 + i] = (uint32_t)(jh - jl);
         if (jh - jl > wp.cap) atomicAdd(&ws.flags[1], 1ull);
     }
-    xe = x + jtot * Lr;
+    xe = x + jtot * L;
     return g0 + ie;
 }
 
@@ -1447,17 +1541,29 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + g0 * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
-    const uint64_t *rs = kAlgo == 4 && wp.rsum ? wp.rsum + g0 * (uint64_t)wp.seg_words / 64 : nullptr;
+    const uint64_t *rs = wp.rsum ? wp.rsum + g0 * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t xprev = 0;
     bool have = false;
+    // entries and predecessor exits prefetched 64 segments at a time (lane l:
+    // segment gb + l), so settled segments cost no dependent load each; this
+    // pass rewrites only segments it has passed
+    uint64_t gb = 0, eR = 0, xR = 0;
+    bool pref = false;
     for (uint64_t g = max(g0 + 1, (uint64_t)ws.flags[2]); g < g1; ++g) {
-        const uint64_t x = have ? xprev : ws.X[g - 1];
+        if (!pref || g - gb >= 64) {
+            gb = g;
+            pref = true;
+            eR = g + lane < g1 ? ws.E[g + lane] : 0ull;
+            xR = g + lane < g1 ? ws.X[g + lane - 1] : 0ull;
+        }
+        const uint32_t i = (uint32_t)(g - gb);
+        const uint64_t x = have ? xprev : rdlane64(xR, i);
         have = false;
-        if (ws.E[g] == x) continue;
-        if constexpr (kAlgo == 4) {
+        if (rdlane64(eR, i) == x) continue;
+        if (rs) {
             uint64_t xe;
-            const uint64_t ge = rs ? serial_run(st, wp, ws, B, rs, g0, g1, g, x, len, lane, xe) : g;
-            if (ge > g) {  // segments g .. ge-1 lie wholly inside one repeat run
+            const uint64_t ge = serial_run<kAlgo>(st, wp, ws, B, rs, g0, g1, g, x, len, lane, xe);
+            if (ge > g) {  // segments g .. ge-1 lie wholly inside one quiet run
                 xprev = xe;
                 have = true;
                 g = ge - 1;
@@ -1736,7 +1842,7 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
     } else if constexpr (kAlgo == 6) {
         // SeqCDC: bit p = (b[p] > b[p-1]) (increasing) or (b[p] < b[p-1]).
         uint32_t last = p0 >= 1 ? base[p0 - 1] : 0u;
-        uint64_t acc = 0;
+        uint64_t acc = 0, wlast = 0;
         for_chunks(base, len, p0, p1, [&](const uint4 &cur, uint64_t a) {
             const uint32_t sh = (uint32_t)((a - p0) & 63);
 #pragma unroll
@@ -1747,9 +1853,14 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             }
             if (sh == 48 || a + 16 >= p1) {
                 out[(a - p0) >> 6] = acc;
+                wlast = acc;
                 acc = 0;
             }
         });
+        if (fine && wp.rsum) {  // quiet-run summary: words without an in-direction pair
+            const uint64_t full = __ballot(wlast == 0);
+            if (threadIdx.x == 0) wp.rsum[(pc.wbase >> 6) + it] = full;
+        }
     } else {
         // Leap eligibility of the 5-byte window ending at p (bytes [a-16, a+16)).
         uint4 prev = p0 >= 16 ? load16_guarded(base, p0 - 16, len) : make_uint4(0, 0, 0, 0);
@@ -1814,51 +1925,67 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     const uint8_t *base = st.ptrs[pc.si];
     const uint64_t w = (1ull << wp.piece_log2) >> 6;  // bytes per lane (a multiple of 64)
     const uint64_t p0 = pc.off + lane * w;
-    if (p0 >= len) return;
+    uint32_t qm = 0, qa = 0;  // bit i: word i of the lane's range has no hit / only hits (quiet runs)
+    if (p0 < len) {
     const uint64_t p1 = min(p0 + w, len);
-    uint64_t *out = wp.bm + (pc.wbase + lane * (w >> 6));
-    const uint32_t rmask = (uint32_t)wp.rabin_mask, tsh = wp.rabin_shift - 32;
-    uint32_t lo = 0, hi = 0;
-    auto step16 = [&](const uint4 &cur, const uint4 &old, uint32_t &bits, int sh, bool test) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint64_t o = tout[byte_of(old, j) * kRabinReps];
-            lo ^= (uint32_t)o;
-            hi ^= (uint32_t)(o >> 32);
-            const uint64_t m = tmod[(hi >> tsh) * kRabinReps];
-            hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
-            lo = ((lo << 8) | byte_of(cur, j)) ^ (uint32_t)m;
-            if (test) bits |= min(lo & rmask, 1u) << (sh + j);
+        uint64_t *out = wp.bm + (pc.wbase + lane * (w >> 6));
+        const uint32_t rmask = (uint32_t)wp.rabin_mask, tsh = wp.rabin_shift - 32;
+        uint32_t lo = 0, hi = 0;
+        auto step16 = [&](const uint4 &cur, const uint4 &old, uint32_t &bits, int sh, bool test) {
+    #pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t o = tout[byte_of(old, j) * kRabinReps];
+                lo ^= (uint32_t)o;
+                hi ^= (uint32_t)(o >> 32);
+                const uint64_t m = tmod[(hi >> tsh) * kRabinReps];
+                hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
+                lo = ((lo << 8) | byte_of(cur, j)) ^ (uint32_t)m;
+                if (test) bits |= min(lo & rmask, 1u) << (sh + j);
+            }
+        };
+        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0;  // chunks 48, 32, 16 bytes back
+        uint32_t dummy = 0;
+        for (uint64_t a = p0 >= CDC_RABIN_WINDOW ? p0 - CDC_RABIN_WINDOW : p0; a < p0; a += 16) {
+            const uint4 cur = load16_guarded(base, a, len);
+            step16(cur, c0, dummy, 0, false);
+            c0 = c1;
+            c1 = c2;
+            c2 = cur;
         }
-    };
-    uint4 c0 = make_uint4(0, 0, 0, 0), c1 = c0, c2 = c0;  // chunks 48, 32, 16 bytes back
-    uint32_t dummy = 0;
-    for (uint64_t a = p0 >= CDC_RABIN_WINDOW ? p0 - CDC_RABIN_WINDOW : p0; a < p0; a += 16) {
-        const uint4 cur = load16_guarded(base, a, len);
-        step16(cur, c0, dummy, 0, false);
-        c0 = c1;
-        c1 = c2;
-        c2 = cur;
+        uint4 n0 = load16_guarded(base, p0, len), n1 = load16_guarded(base, p0 + 16, len);
+        uint4 n2 = load16_guarded(base, p0 + 32, len), n3 = load16_guarded(base, p0 + 48, len);
+        for (uint64_t a = p0; a < p1; a += 64) {
+            const uint4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
+            if (a + 64 < p1) {
+                n0 = load16_guarded(base, a + 64, len);
+                n1 = load16_guarded(base, a + 80, len);
+                n2 = load16_guarded(base, a + 96, len);
+                n3 = load16_guarded(base, a + 112, len);
+            }
+            uint32_t b0 = 0, b1 = 0;
+            step16(q0, c0, b0, 0, true);
+            step16(q1, c1, b0, 16, true);
+            step16(q2, c2, b1, 0, true);
+            step16(q3, q0, b1, 16, true);
+            c0 = q1;
+            c1 = q2;
+            c2 = q3;
+            const uint64_t hits = ~(((uint64_t)b1 << 32) | b0);  // bit set = window hit
+            out[(a - p0) >> 6] = hits;
+            qm |= (uint32_t)(hits == 0) << ((a - p0) >> 6);
+            qa |= (uint32_t)(hits == ~0ull) << ((a - p0) >> 6);
+        }
     }
-    uint4 n0 = load16_guarded(base, p0, len), n1 = load16_guarded(base, p0 + 16, len);
-    uint4 n2 = load16_guarded(base, p0 + 32, len), n3 = load16_guarded(base, p0 + 48, len);
-    for (uint64_t a = p0; a < p1; a += 64) {
-        const uint4 q0 = n0, q1 = n1, q2 = n2, q3 = n3;
-        if (a + 64 < p1) {
-            n0 = load16_guarded(base, a + 64, len);
-            n1 = load16_guarded(base, a + 80, len);
-            n2 = load16_guarded(base, a + 96, len);
-            n3 = load16_guarded(base, a + 112, len);
+    if (wp.rsum) {  // the lanes' quiet bits into summary bytes (nw words per lane, 8 / nw lanes per byte)
+        const uint32_t nw = (uint32_t)(w >> 6), gl = 8 / nw;
+        uint32_t v = (qm | qa << 8) << (nw * (lane & (gl - 1)));
+        for (uint32_t o = 1; o < gl; o <<= 1) v |= (uint32_t)__shfl_xor((int)v, (int)o);
+        if ((lane & (gl - 1)) == 0) {  // kinds interleaved: summary word sk of kind q at rsum[2 sk + q]
+            const uint64_t W = pc.wbase + lane * nw;
+            uint8_t *b = reinterpret_cast<uint8_t *>(wp.rsum) + (W >> 6) * 16 + ((W >> 3) & 7);
+            b[0] = (uint8_t)v;
+            b[8] = (uint8_t)(v >> 8);
         }
-        uint32_t b0 = 0, b1 = 0;
-        step16(q0, c0, b0, 0, true);
-        step16(q1, c1, b0, 16, true);
-        step16(q2, c2, b1, 0, true);
-        step16(q3, q0, b1, 16, true);
-        c0 = q1;
-        c1 = q2;
-        c2 = q3;
-        out[(a - p0) >> 6] = ~(((uint64_t)b1 << 32) | b0);  // bit set = window hit
     }
 }
 
@@ -1954,8 +2081,12 @@ __global__ __launch_bounds__(256) void lbits_kernel(const StreamTable st, const 
             }
         }
         uint64_t *out = wp.bm + (pc.wbase + lidx) * 2;
-        out[0] = ((uint64_t)pr[1] << 32) | pr[0];
-        out[1] = ((uint64_t)se[1] << 32) | se[0];
+        const uint64_t prw = ((uint64_t)pr[1] << 32) | pr[0], sew = ((uint64_t)se[1] << 32) | se[0];
+        out[0] = prw;
+        out[1] = sew;
+        // quiet-run summary: words whose windows are all eligible
+        const uint64_t full = __ballot((prw & sew) == ~0ull);
+        if (wp.rsum && lane == 0) wp.rsum[(pc.wbase >> 6) + it] = full;
     }
 }
 
@@ -2205,6 +2336,16 @@ hipError_t dispatch(int which, const StreamTable &st, const WalkParams &wp, cons
 }
 
 }  // namespace
+
+bool bits_write_summary(const WalkParams &wp) {
+    if (!wp.wave || !wp.nbm || wp.piece_log2 < 12 || wp.piece_log2 > 15) return false;
+    switch (wp.algo) {
+        case 2: return wp.rabin_mask <= 0xFFFFFFFFull && wp.rabin_shift >= 32;  // rbits_kernel
+        case 4: case 5: return wp.bits_fine != 0;                               // ubits / lbits_kernel
+        case 6: return wp.bits_fine != 0;                                       // bits_kernel<6>, fine
+        default: return false;
+    }
+}
 
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
     if (!st.total_spans || !wp.nbm) return hipSuccess;

@@ -70,11 +70,14 @@ struct WalkParams {
     // block, jt8[b * 24 + e] (u16): < 24 = entry into block b + 1, >= 512 =
     // accepted at 512 b + (v - 512).
     uint16_t *jt8;
-    // UltraCDC wave walks: one bit per repeat-bitmap word, bit k & 63 of
-    // rsum[k >> 6] (k = segment g's word index + g * seg_words): all 64
-    // positions of the word are 8-byte repeats.  A chain inside a long run
-    // of repeats (zero-filled or 8-byte-periodic regions) takes its LEST
-    // chunks many at a time (ultra_run) instead of one wcut per chunk.
+    // Wave walks: one "quiet" bit per bitmap word, bit k & 63 of rsum[k >> 6]
+    // (k = segment g's word index + g * seg_words), written by the bitmap
+    // pass: Rabin no hit, SeqCDC no in-direction pair, UltraCDC all 8-byte
+    // repeats, LeapCDC all windows eligible.  Chains inside long quiet runs
+    // (zero-filled or constant regions), where every chunk has one fixed
+    // length, take the run's chunks many at a time (walk.hip quiet_run).
+    // nullptr when the bitmap pass in use does not write it
+    // (bits_write_summary).
     uint64_t *rsum;
 };
 
@@ -103,6 +106,9 @@ constexpr uint32_t kMaxFixRounds = 16;  // flag blocks allocated after the main 
 constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
 
 // Bitmap mode: the predicate bitmaps of every segment (wave per segment).
+// Whether the bitmap pass launch_bits picks for wp writes the quiet-run
+// summary (wp.rsum may be non-null only then).
+bool bits_write_summary(const WalkParams &wp);
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s);
 // Link mode: candidate lists (wave per segment), then the links (lane per candidate).
 hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t s);

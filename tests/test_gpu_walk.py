@@ -299,34 +299,56 @@ def repeat_run_stream(n, seed):
     return d
 
 
-@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (512, 2048, 16384), (2048, 8192, 65536),
-                                   (16384, 65536, 524288)])
-def test_ultra_repeat_runs_exact(sizes):
-    """UltraCDC over long repeat runs in a 3-stream device batch (40 MiB, 24 MiB
-    of zeros, 7 MiB + 1): bit-exact vs the oracle."""
+QUIET_SIZES = [(4096, 8192, 16384), (512, 2048, 16384), (2048, 8192, 65536), (16384, 65536, 524288)]
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("sizes", QUIET_SIZES)
+def test_quiet_runs_exact(algo, sizes):
+    """Every walk rule over long zero-filled / constant / 8-byte-periodic runs
+    at unaligned offsets (quiet runs: walk.hip quiet_run) in a 3-stream device
+    batch (40 MiB, 24 MiB of zeros, 7 MiB + 1): bit-exact vs the oracle."""
     import torch
     lens = [40 << 20, 24 << 20, (7 << 20) + 1]
     hosts = [repeat_run_stream(lens[0], 31), np.zeros(lens[1], dtype=np.uint8), repeat_run_stream(lens[2], 32)]
     devs = [torch.from_numpy(h).to("cuda:0") for h in hosts]
-    ch = chunker("ultra", sizes)
+    ch = chunker(algo, sizes)
     cap = ch.batch_max_chunks(lens)
     out = torch.empty((cap, 2), dtype=torch.int64, device="cuda:0")
     torch.cuda.synchronize()
     first = ch.chunk_batch_device([d.data_ptr() for d in devs], lens, out.data_ptr(), cap)
     got = out[:first[-1]].cpu().numpy().astype(np.uint64)
     for i, h in enumerate(hosts):
-        assert_same(got[first[i]:first[i + 1]], oracle.cdc("ultra", h, *sizes), f"ultra {sizes} stream {i}")
+        assert_same(got[first[i]:first[i + 1]], oracle.cdc(algo, h, *sizes), f"{algo} {sizes} stream {i}")
 
 
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("walk,ahead", [("13,2", "16,1"), ("17,1", "0,64")])
-def test_ultra_repeat_runs_serial_pass(walk, ahead, monkeypatch):
-    """The in-order pass over repeat runs (segment lists written per run,
+def test_quiet_runs_serial_pass(algo, walk, ahead, monkeypatch):
+    """The in-order pass over quiet runs (segment lists written per run,
     serial_run): schedules that leave most segments to it."""
     import chunkfs_amd as c
     monkeypatch.setenv("CHUNKFS_AMD_WALK", walk)
     monkeypatch.setenv("CHUNKFS_AMD_AHEAD", ahead)
-    sizes = (4096, 8192, 16384)
-    ch = c.UltraChunker(c.SizeParams(*sizes))
-    for data in (np.zeros((16 << 20) + 77, dtype=np.uint8), repeat_run_stream(24 << 20, 33)):
-        assert_same(ch.chunk_array(data), oracle.cdc("ultra", data, *sizes), f"ultra serial {walk} {ahead}")
+    sizes = SIZES[algo][0]
+    cls = {"rabin": c.RabinChunker, "ultra": c.UltraChunker, "leap": c.LeapChunker}.get(algo)
+    ch = cls(c.SizeParams(*sizes)) if cls else c.SeqChunker(0, c.SizeParams(*sizes))
+    zr = oracle.splitmix64_bytes((16 << 20) + 77, 34)
+    zr[123457:] = 0  # random, then zeros from an arbitrary phase
+    for data in (zr, repeat_run_stream(24 << 20, 33)):
+        assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} serial {walk} {ahead}")
     ch.close()
+
+
+def test_quiet_summary_off_paths(monkeypatch):
+    """Bitmap passes that write no quiet summary (CHUNKFS_AMD_BITS_FINE=0: the
+    lane-per-range kernels) leave the quiet runs off: still exact."""
+    import chunkfs_amd as c
+    monkeypatch.setenv("CHUNKFS_AMD_BITS_FINE", "0")
+    data = repeat_run_stream(12 << 20, 35)
+    for algo in ("ultra", "leap", "seq"):
+        sizes = SIZES[algo][0]
+        cls = {"ultra": c.UltraChunker, "leap": c.LeapChunker}.get(algo)
+        ch = cls(c.SizeParams(*sizes)) if cls else c.SeqChunker(0, c.SizeParams(*sizes))
+        assert_same(ch.chunk_array(data), oracle.cdc(algo, data, *sizes), f"{algo} bits_fine=0")
+        ch.close()

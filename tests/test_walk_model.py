@@ -352,3 +352,61 @@ def test_ultra_repeat_runs_model(sizes):
     assert np.array_equal(np.array(got, dtype=np.uint64).reshape(-1, 2), ref)
     if mx >= Lr:
         assert jumped > 0
+
+
+def quiet_run(loud, c, n, lim, L, lo, hi):
+    """walk.hip quiet_run over a boolean 'loud' array (generic form of ultra_run)."""
+    if c >= lim or n - c < L:
+        return 0
+    kmax = min((n - c) // L, (lim - c + L - 1) // L)
+    a, tail = c + lo, hi - lo
+    need = a + (kmax - 1) * L + tail + 1
+    z = np.nonzero(loud[a:need])[0]
+    b = a + int(z[0]) if z.size else need
+    return min(kmax, (b - a - tail + L - 1) // L) if b > a + tail else 0
+
+
+def walk_with_quiet_runs(cut, loud, n, L, lo, hi):
+    """The wave walks' loop: after two chunks of exactly L in a row, take the
+    quiet run's chunks at once (take_run)."""
+    got, pos, pq, jumped = [], 0, False, 0
+    while pos < n:
+        d = cut(pos)
+        got.append((pos, d))
+        pos += d
+        q = d == L
+        if q and pq:
+            k = quiet_run(loud, pos, n, n, L, lo, hi)
+            got += [(pos + j * L, L) for j in range(k)]
+            pos += k * L
+            jumped += k
+            pq = k != 0
+        else:
+            pq = q
+    return np.array(got, dtype=np.uint64).reshape(-1, 2), jumped
+
+
+@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (2048, 8192, 65536)])
+def test_quiet_runs_model_seq_leap(sizes):
+    """SeqCDC (L = max over pair-free runs) and LeapCDC (L = min over
+    all-eligible runs) with quiet-run jumps cut exactly where the oracle does
+    on zero-filled / constant regions at unaligned offsets."""
+    mn, avg, mx = sizes
+    n = (1 << 20) + 4321
+    d = repeat_regions(n, 21)
+    # SeqCDC, increasing mode
+    Ls, Ts, Js = P["CDC_SEQ_LENGTH"], P["CDC_SEQ_JUMP_TRIGGER"], P["CDC_SEQ_JUMP_SIZE"]
+    y = np.zeros(n, dtype=bool)
+    y[1:] = d[1:] > d[:-1]
+    got, jumped = walk_with_quiet_runs(lambda s: wcut_seq(y, s, n - s, mn, mx, Ls, Ts, Js), y, n, mx, mn - 1, mx - 1)
+    assert np.array_equal(got, oracle.cdc("seq", d, mn, avg, mx))
+    assert jumped > 0
+    # LeapCDC
+    prim, sec = leap_bitmaps(d, mn, avg)
+    tabs = leap_tables(prim, sec)
+    t8 = block_tables(tabs)
+    W = P["CDC_LEAP_WINDOWS"]
+    loud = ~(prim & sec)
+    got, jumped = walk_with_quiet_runs(lambda s: wcut_leap(prim, sec, tabs, t8, s, n - s, mn, mx), loud, n, mn,
+                                       mn - W, mn - 1)
+    assert np.array_equal(got, oracle.cdc("leap", d, mn, avg, mx))
