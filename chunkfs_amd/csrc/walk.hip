@@ -1370,27 +1370,55 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
 // rewalk() for one wave (wave-uniform chain; lane 0 writes): re-walk segment g
 // from x until the new chain meets the old one (<= kNew new starts, kept in
 // the wave's LDS slots), else a full walk.  xo = the segment's exit after it.
+// Up to kWNew new starts are kept in registers (lane k & 63 of nb[k >> 6])
+// before a meeting point; the old list is checked 64 entries at a time (lane
+// l holds old start j0 + l: a meeting is one ballot), and the list is
+// rewritten by all lanes.  128 covers a whole segment at the default sizes, so
+// a re-walk without a meeting point does not walk the segment twice (SeqCDC's
+// fix-up rounds per GiB at 4/8/16 KiB: 8 held starts 0.37 ms, 128: 0.29;
+// profiles/r03_walk/r03as_rewalk_held_starts.log).
+#ifndef CDC_WNEW  // (experiment builds, tools/build_variants.py)
+#define CDC_WNEW 128
+#endif
+constexpr uint32_t kWNew = CDC_WNEW;
+static_assert(kWNew <= 128, "two registers of held starts");
+
+// Moves list[j .. lim) to list[m ..) (entries at or past cap dropped), 64 at a
+// time, in the order that never overwrites an entry before it is read.
+__device__ void shift_list(uint64_t *list, uint32_t j, uint32_t lim, uint32_t m, uint32_t cap, uint32_t lane) {
+    const uint32_t cnt = lim - j, nch = (cnt + 63) / 64;
+    for (uint32_t i = 0; i < nch; ++i) {
+        const uint32_t ci = m > j ? nch - 1 - i : i;
+        const uint32_t k = ci * 64 + lane;
+        const uint64_t v = k < cnt ? list[j + k] : 0ull;
+        if (k < cnt && m + k < cap) list[m + k] = v;
+    }
+}
+
 template <int kAlgo>
 __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, const WBm &B, const uint64_t *rs,
-                        const WalkParams &wp, const WalkState &ws, uint64_t *nb, uint32_t lane, uint64_t &xo) {
+                        const WalkParams &wp, const WalkState &ws, uint32_t lane, uint64_t &xo) {
     uint64_t *list = ws.list + g * wp.cap;
     const uint32_t n_old = ws.N[g];
     const uint32_t lim = min(n_old, wp.cap);
     const uint64_t x_old = ws.X[g];
     uint64_t c = x;
-    uint32_t m = 0, j = 0;
+    uint32_t m = 0, j0 = 0;
+    uint64_t ow = lane < lim ? list[lane] : ~0ull;  // old starts j0 + lane
+    uint64_t nb0 = 0, nb1 = 0;                      // new starts lane, 64 + lane
     int pk = -1;
-    while (c < seg_end && m < kNew) {
-        while (j < lim && list[j] < c) ++j;
-        if (j < lim && list[j] == c) {  // meets the old chain at old start j
+    while (c < seg_end && m < kWNew) {
+        while (j0 + 64 < lim && rdlane64(ow, 63) < c) {
+            j0 += 64;
+            ow = j0 + lane < lim ? list[j0 + lane] : ~0ull;
+        }
+        const uint64_t hit = __ballot(ow == c);
+        if (hit) {  // meets the old chain at old start j
+            const uint32_t j = j0 + (uint32_t)__builtin_ctzll(hit);
+            if (m != j) shift_list(list, j, lim, m, wp.cap, lane);
+            if (lane < m && lane < wp.cap) list[lane] = nb0;
+            if (64 + lane < m && 64 + lane < wp.cap) list[64 + lane] = nb1;
             if (lane == 0) {
-                if (m < j) {
-                    for (uint32_t k = j; k < lim; ++k) list[m + k - j] = list[k];
-                } else if (m > j) {
-                    for (uint32_t k = lim; k-- > j;)
-                        if (m + k - j < wp.cap) list[m + k - j] = list[k];
-                }
-                for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
                 ws.E[g] = x;
                 ws.N[g] = m + (n_old - j);
                 if (m + (n_old - j) > wp.cap) atomicAdd(&ws.flags[1], 1ull);
@@ -1398,7 +1426,10 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
             xo = x_old;
             return false;
         }
-        if (lane == 0) nb[m] = c;
+        if (lane == (m & 63)) {
+            if (m < 64) nb0 = c;
+            else nb1 = c;
+        }
         ++m;
         const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
         c += d;
@@ -1406,17 +1437,19 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
         uint64_t L;
         if (kind >= 0 && (!kQuietTwice<kAlgo> || kind == pk) && rs && c < seg_end &&
             quiet_run_k<kAlgo>(kind, B, rs, c, len, seg_end, wp, lane, L) >= 2) {
-            m = kNew + 1;
+            m = kWNew + 1;
             break;
         }
         pk = kind;
     }
-    if (c >= seg_end && m <= kNew) {  // the whole segment in <= kNew starts, no meeting point
+    if (c >= seg_end && m <= kWNew) {  // the whole segment in <= kWNew starts, no meeting point
+        if (lane < m && lane < wp.cap) list[lane] = nb0;
+        if (64 + lane < m && 64 + lane < wp.cap) list[64 + lane] = nb1;
         if (lane == 0) {
-            for (uint32_t k = 0; k < m; ++k) list[k] = nb[k];
             ws.E[g] = x;
             ws.N[g] = m;
             ws.X[g] = c;
+            if (m > wp.cap) atomicAdd(&ws.flags[1], 1ull);
         }
         xo = c;
         return c != x_old;
@@ -1448,7 +1481,6 @@ template <int kAlgo>
 __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
     if (ws.gate && *ws.gate == 0) return;  // the previous round settled everything
     constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
-    __shared__ uint64_t nbuf[4 * kNew];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (g >= st.total_spans) return;
@@ -1465,14 +1497,13 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
-    uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
     const uint64_t *rs = wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t gg = g;
     for (uint32_t k = 0;; ++k) {
         const uint64_t seg_end = min(off + span, len);
         if (lane == 0) atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
         uint64_t xo;
-        if (!wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, nb, lane, xo)) break;
+        if (!wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, lane, xo)) break;
         if (seg_end >= len) break;  // the stream's last segment: no successor
         if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
             if (lane == 0) {
@@ -1529,7 +1560,6 @@ __device__ uint64_t serial_run(const StreamTable &st, const WalkParams &wp, cons
 template <int kAlgo>
 __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
     constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
-    __shared__ uint64_t nbuf[4 * kNew];
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t si = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (si >= st.n) return;
@@ -1540,7 +1570,6 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
                 kAlgo == 5 ? wp.jt + g0 * (uint64_t)wp.seg_words * 24 : nullptr,
                 lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + g0 * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
-    uint64_t *nb = nbuf + (threadIdx.x >> 6) * kNew;
     const uint64_t *rs = wp.rsum ? wp.rsum + g0 * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t xprev = 0;
     bool have = false;
@@ -1573,7 +1602,7 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
         const uint64_t off = (g - g0) << st.span_log2;
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
         uint64_t xo;
-        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, rs, wp, ws, nb, lane, xo);
+        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, rs, wp, ws, lane, xo);
         xprev = xo;
         have = true;
     }
