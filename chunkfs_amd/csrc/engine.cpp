@@ -902,8 +902,8 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     HIP_TRY(hipMemsetAsync(rf, 0, (size_t)R * 4 * 8, s));
     HIP_TRY(hipMemset2DAsync(rf + 2, 32, 0xFF, 8, R, s));  // lowest segment whose exit changed
     uint64_t rewalked = 0, round_errors = 0;
-    bool settled = false;
-    uint32_t launched = 0;
+    bool settled = false, quiet_stop = false;
+    uint32_t launched = 0, last_round = 0;
     while (launched < R && !settled) {
         const uint32_t end = launched + kGroup < R ? launched + kGroup : R;
         for (uint32_t r = launched; r < end; ++r) {
@@ -925,11 +925,29 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         launched = end;
         HIP_TRY(hipMemcpyAsync(h_rf, rf, (size_t)launched * 4 * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        for (uint32_t r = 0; r < launched && !settled; ++r) settled = h_rf[4 * r] == 0;
+        // The first round that settled everything, or whose changed exits
+        // were mostly quiet-run re-walks (zero-filled / constant regions:
+        // chains there keep their phase, so each round moves the true one a
+        // single segment; the in-order pass takes such a region in one go).
+        // Later rounds of the group returned at once on the device (the same
+        // rule, walk.hip round_stops).
+        for (uint32_t r = 0; r < launched; ++r) {
+            const uint64_t ch = h_rf[4 * r], q = h_rf[4 * r + 3] >> 32;
+            if (ch == 0) {
+                settled = true;
+                break;
+            }
+            if (2 * q >= ch) {
+                last_round = r;
+                quiet_stop = true;
+                break;
+            }
+        }
+        if (quiet_stop) break;
     }
     for (uint32_t r = 0; r < launched; ++r) {
         round_errors += h_rf[4 * r + 1];
-        rewalked += h_rf[4 * r + 3];
+        rewalked += h_rf[4 * r + 3] & 0xFFFFFFFFull;
     }
     if (diag) {
         std::fprintf(stderr, "  walkdiag rounds %u settled %d:", launched, (int)settled);
@@ -940,7 +958,8 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     // Chains that never merge (periodic data): one exact in-order pass from
     // the lowest segment the last round changed.
     if (!settled) {
-        HIP_TRY(hipMemcpyAsync(wst_.flags + 2, rf + 4 * (R - 1) + 2, 8, hipMemcpyDeviceToDevice, s));
+        const uint32_t lr = quiet_stop ? last_round : launched - 1;  // the last round that ran
+        HIP_TRY(hipMemcpyAsync(wst_.flags + 2, rf + 4 * lr + 2, 8, hipMemcpyDeviceToDevice, s));
         HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
     }
     (void)lap("fixup");

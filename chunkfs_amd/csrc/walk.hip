@@ -662,10 +662,18 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
 // instead of one round per segment.  Scheduling reads only the snapshots, so a
 // run-ahead write of E[g+1] never makes lane g+1 re-walk concurrently.
 
+// A fix-up round runs only while the previous one changed exits and those
+// were not mostly quiet-run re-walks (the host applies the same rule and hands
+// a quiet-dominated stream to the in-order pass; WalkState::flags[3] counts
+// quiet re-walks in its high half).
+__device__ __forceinline__ bool round_stops(const unsigned long long *gate) {
+    return gate && (gate[0] == 0 || 2 * (gate[3] >> 32) >= gate[0]);
+}
+
 template <int kAlgo, bool kBits>
 __global__ __launch_bounds__(kWalkBlock) void fix_kernel(const StreamTable st, const WalkParams wp,
                                                          const WalkState ws) {
-    if (ws.gate && *ws.gate == 0) return;  // the previous round settled everything
+    if (round_stops(ws.gate)) return;  // the previous round settled everything (or went quiet)
     __shared__ uint64_t tab[768];
     __shared__ __attribute__((aligned(16))) uint8_t win[kWalkBlock * kSlot];
     __shared__ uint64_t nbuf[kWalkBlock * kNew];
@@ -1397,7 +1405,8 @@ __device__ void shift_list(uint64_t *list, uint32_t j, uint32_t lim, uint32_t m,
 
 template <int kAlgo>
 __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, const WBm &B, const uint64_t *rs,
-                        const WalkParams &wp, const WalkState &ws, uint32_t lane, uint64_t &xo) {
+                        const WalkParams &wp, const WalkState &ws, uint32_t lane, uint64_t &xo, bool &qr) {
+    qr = false;  // set: the new chain entered a quiet run (its phase will not merge)
     uint64_t *list = ws.list + g * wp.cap;
     const uint32_t n_old = ws.N[g];
     const uint32_t lim = min(n_old, wp.cap);
@@ -1438,6 +1447,7 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
         if (kind >= 0 && (!kQuietTwice<kAlgo> || kind == pk) && rs && c < seg_end &&
             quiet_run_k<kAlgo>(kind, B, rs, c, len, seg_end, wp, lane, L) >= 2) {
             m = kWNew + 1;
+            qr = true;
             break;
         }
         pk = kind;
@@ -1479,7 +1489,7 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
 // ahead into unscheduled successors), wave-cooperative re-walks.
 template <int kAlgo>
 __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
-    if (ws.gate && *ws.gate == 0) return;  // the previous round settled everything
+    if (round_stops(ws.gate)) return;  // the previous round settled everything (or went quiet)
     constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1503,7 +1513,12 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
         const uint64_t seg_end = min(off + span, len);
         if (lane == 0) atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
         uint64_t xo;
-        if (!wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, lane, xo)) break;
+        bool qr;
+        const bool changed = wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, lane, xo, qr);
+        // (quiet re-walks counted in the high half: the host hands rounds of
+        // mostly phase-locked quiet segments to the in-order pass early)
+        if (qr && changed && lane == 0) atomicAdd(&ws.flags[3], 1ull << 32);
+        if (!changed) break;
         if (seg_end >= len) break;  // the stream's last segment: no successor
         if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
             if (lane == 0) {
@@ -1602,7 +1617,8 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
         const uint64_t off = (g - g0) << st.span_log2;
         const uint64_t seg_end = min(off + (1ull << st.span_log2), len);
         uint64_t xo;
-        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, rs, wp, ws, lane, xo);
+        bool qr;
+        (void)wrewalk<kAlgo>(x, g, seg_end, len, B, rs, wp, ws, lane, xo, qr);
         xprev = xo;
         have = true;
     }
