@@ -82,14 +82,21 @@ def parse(argv=None):
                    help="bytes of the bench stream the config-5 size sweep chunks")
     p.add_argument("--no-config5", action="store_true",
                    help="skip the config-5 (16 GiB, walk rules at 2/8/64 KiB, strong scaling) sub-object")
+    p.add_argument("--config5-streams", type=int, default=16,
+                   help="config 5: total streams, split across ranks (strong scaling)")
+    p.add_argument("--config5-stream-bytes", type=int, default=1 << 30, help="config 5: bytes per stream")
     p.add_argument("--config5-check", type=int, default=64 << 20,
                    help="config 5: bytes of rank 0's first stream checked against the oracle")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU launcher test only
     # Multi-rank rehearsal on a box with fewer GPUs than ranks (tests only):
-    # gloo collectives, ranks mapped onto the visible devices round-robin, and
-    # every rank checks its own first streams against the oracle.
-    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl", help=argparse.SUPPRESS)
+    # ranks mapped onto the visible devices round-robin, and every rank checks
+    # its own first streams against the oracle.
+    # The only collectives are the barrier and the scalar timing / byte-count
+    # reductions (no data-path collective): gloo on the host by
+    # default; nccl (= RCCL) reduces on the devices instead.
+    p.add_argument("--dist-backend", choices=["gloo", "nccl"], default="gloo",
+                   help="backend of the barrier and the scalar reductions (default gloo)")
     p.add_argument("--share-device", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--rank-parity", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args(argv)
@@ -269,7 +276,8 @@ def config4_leg(args, eng, rank, world, red_dev):
 
 def config5_leg(args, eng, rank, world, red_dev):
     """Config 5 (BASELINE configs[4]) at every N: 16 GiB of synthetic data as
-    16 independent 1 GiB streams (stream i: seed 5000+i) split across the ranks
+    16 independent 1 GiB streams (--config5-streams x --config5-stream-bytes;
+    stream i: seed 5000+i) split across the ranks
     (strong scaling, no collective), UltraCDC and LeapCDC (plus Rabin and
     SeqCDC) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg.
     Per (rule, sizes): one warm-up pass, then one pass bracketed by a barrier
@@ -283,7 +291,8 @@ def config5_leg(args, eng, rank, world, red_dev):
     import torch.distributed as dist
     import chunkfs_amd as cfa
     from chunkfs_amd import sharding
-    shard = sharding.batch_shard(rank, world, 16, 1 << 30)
+    nst, sbytes = args.config5_streams, args.config5_stream_bytes
+    shard = sharding.batch_shard(rank, world, nst, sbytes)
     dev = eng.dev
     bufs = []
     for n, sd in zip(shard.lens, shard.seeds):
@@ -297,7 +306,7 @@ def config5_leg(args, eng, rank, world, red_dev):
     if rank == 0 and not args.no_parity and lens:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        host0 = bufs[0][:args.config5_check].cpu().numpy()
+        host0 = bufs[0][:min(args.config5_check, lens[0])].cpu().numpy()
     res = {}
     for avg in (2048, 8192, 65536):
         sz = cfa.SizeParams(avg // 4, avg, avg * 8)
@@ -329,7 +338,8 @@ def config5_leg(args, eng, rank, world, red_dev):
             ch.close()
             del out
     del bufs
-    return {"workload": f"config5: 16 x 1 GiB synthetic streams split across {world} GPU(s)", "scaling": "strong",
+    return {"workload": f"config5: {nst} x {sbytes} B synthetic streams split across {world} GPU(s)",
+            "scaling": "strong",
             "streams_per_gpu": len(lens), "bytes_per_gpu": sum(lens),
             "frac_definition": "per-GPU bytes / max-over-ranks time / 8 TB/s",
             "parity_definition": f"rank 0, stream 0, the chunks inside its first {args.config5_check} B" if oracle

@@ -256,6 +256,11 @@ class RabinChunker(_SizedChunker):
     a degree-53 polynomial, cut where digest & (2^round(log2 avg) - 1) == 0."""
     _algo, _name = "rabin", "RabinChunker"
 
+    def set_poly(self, poly):
+        """Install another polynomial (cdc_set_rabin_poly; degree 9..56): the
+        one-call hook for the crate's ChunkerParams once its source exists."""
+        check(lib().cdc_set_rabin_poly(self._h, int(poly)))
+
 
 class UltraChunker(_SizedChunker):
     """UltraCDC (src/chunkers/ultra.rs:30-44): 8-byte Hamming distance to 0xAA..,
@@ -347,8 +352,9 @@ class StreamWriter:
     cdc_write_segment / cdc_write_finish): ChunkStorage::write_from_stream
     (storage.rs:105-137) with StorageWriter::write per segment and
     StorageWriter::flush at the end (storage.rs:302-383).  Segments are copied
-    into a pinned ring and uploaded while the caller continues; finish()
-    returns (span lengths in file order, wall seconds since begin)."""
+    into a pinned ring and uploaded while the caller continues; drain()
+    returns the spans that became final so far (each chunked 256 MiB device
+    window), finish() the rest and the wall seconds since begin."""
 
     def __init__(self, chunker):
         self._ch = chunker
@@ -360,6 +366,13 @@ class StreamWriter:
         check(lib().cdc_write_segment(self._ch._h, ptr, n))
         del keep
         self._bytes += n
+
+    def drain(self):
+        """Span lengths final since the last drain (cdc_write_drain), file order."""
+        cap = self._ch.max_chunk_count(self._bytes) + 1
+        out = np.empty(max(cap, 1), dtype=np.uint64)
+        cnt = check(lib().cdc_write_drain(self._ch._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap))
+        return out[:cnt]
 
     def finish(self):
         cap = self._ch.max_chunk_count(self._bytes) + 1
@@ -373,10 +386,12 @@ class StreamWriter:
 
 def host_stats(chunker):
     """cdc_debug_host_stats: chunk_data calls, upload s, total s; streaming
-    write chunking s and segments."""
-    v = (ctypes.c_double * 5)()
-    check(lib().cdc_debug_host_stats(chunker._h, v, 5))
-    return {"calls": int(v[0]), "upload_s": v[1], "total_s": v[2], "write_chunk_s": v[3], "write_segments": int(v[4])}
+    write chunking s and segments; one-launch small-stream calls and how many
+    of them fell back to the regular pipeline."""
+    v = (ctypes.c_double * 7)()
+    check(lib().cdc_debug_host_stats(chunker._h, v, 7))
+    return {"calls": int(v[0]), "upload_s": v[1], "total_s": v[2], "write_chunk_s": v[3], "write_segments": int(v[4]),
+            "small_calls": int(v[5]), "small_fallbacks": int(v[6])}
 
 
 class DedupIndex:

@@ -21,9 +21,9 @@ ALGO = {"fast": 0, "fixed": 1, "rabin": 2, "super": 3, "ultra": 4, "leap": 5, "s
 # Every symbol include/chunkfs_amd.h declares (tests check the export table).
 EXPORTS = [
     "cdc_create", "cdc_create_seq", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
-    "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear",
+    "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear", "cdc_set_rabin_poly",
     "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
-    "cdc_fs_write", "cdc_write_begin", "cdc_write_segment", "cdc_write_finish",
+    "cdc_fs_write", "cdc_write_begin", "cdc_write_segment", "cdc_write_drain", "cdc_write_finish",
     "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
     "cdc_index_create", "cdc_index_destroy", "cdc_index_clear", "cdc_index_insert_device",
     "cdc_index_stats",
@@ -112,6 +112,8 @@ def lib():
     L.cdc_last_error.restype = ctypes.c_char_p
     L.cdc_set_gear.argtypes = [P, u64p]
     L.cdc_set_gear.restype = ctypes.c_int
+    L.cdc_set_rabin_poly.argtypes = [P, ctypes.c_uint64]
+    L.cdc_set_rabin_poly.restype = ctypes.c_int
     L.cdc_chunk_batch_device.argtypes = [P, sz, P, P, P, sz, P, P]
     L.cdc_chunk_batch_device.restype = ctypes.c_int64
     L.cdc_batch_max_chunks.argtypes = [P, sz, u64p]
@@ -124,6 +126,8 @@ def lib():
     L.cdc_write_begin.restype = ctypes.c_int
     L.cdc_write_segment.argtypes = [P, P, sz]
     L.cdc_write_segment.restype = ctypes.c_int
+    L.cdc_write_drain.argtypes = [P, u64p, sz]
+    L.cdc_write_drain.restype = ctypes.c_int64
     L.cdc_write_finish.argtypes = [P, u64p, sz, ctypes.POINTER(ctypes.c_double)]
     L.cdc_write_finish.restype = ctypes.c_int64
     L.cdc_debug_host_stats.argtypes = [P, ctypes.POINTER(ctypes.c_double), sz]

@@ -11,9 +11,9 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libchunkfs_amd.so")
-SOURCES = ["fastcdc.hip", "walk.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "hostpath.cpp", "capi.cpp",
+SOURCES = ["fastcdc.hip", "small.hip", "walk.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "hostpath.cpp", "capi.cpp",
            "index_host.cpp"]
-HEADERS = ["fastcdc.hpp", "walk.hpp", "cdc_kernels.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
+HEADERS = ["fastcdc.hpp", "small.hpp", "walk.hpp", "cdc_kernels.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]

@@ -70,6 +70,11 @@ int cdc_set_gear(cdc_handle_t *h, const uint64_t gear[256]) {
     return h->engine->set_gear(gear);
 }
 
+int cdc_set_rabin_poly(cdc_handle_t *h, uint64_t poly) {
+    if (!h) return (int)bad_handle();
+    return h->engine->set_rabin_poly(poly);
+}
+
 int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
                                const uint8_t *const *d_streams,
                                const uint64_t *lens, cdc_chunk_t *d_out,
@@ -136,6 +141,11 @@ int64_t cdc_write_finish(cdc_handle_t *h, uint64_t *span_lengths, size_t cap, do
     if (n < 0) return n;
     for (size_t i = 0; i < spans.size() && i < cap; ++i) span_lengths[i] = spans[i];
     return n;
+}
+
+int64_t cdc_write_drain(cdc_handle_t *h, uint64_t *span_lengths, size_t cap) {
+    if (!h) return bad_handle();
+    return h->engine->write_drain(span_lengths, cap);
 }
 
 int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n) {

@@ -126,6 +126,13 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         if (cap > 256) cap = 256;
         e->cap_ = (uint32_t)cap;
         e->smax_ = (uint32_t)(span / ((min / 2) * 2) + 2);
+        // Small-stream path (small.hip): its per-lane and per-block record
+        // budgets assume sparse hits, ~2^-10 per position or rarer.
+        const uint32_t pmin = (uint32_t)std::min(__builtin_popcountll(fp.mask_s), __builtin_popcountll(fp.mask_l));
+        e->small_on_ = pmin >= 10;
+        e->small_pmin_ = pmin;
+        if (const char *v = std::getenv("CHUNKFS_AMD_SMALL")) e->small_on_ = e->small_on_ && std::atoi(v) != 0;
+        if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_ZC")) e->small_zc_ = std::atoi(v) != 0;
         char buf[256];
         std::snprintf(buf, sizeof buf,
                       "FastCDC (2020), sizes: SizeParams { min: %u, avg: %u, max: %u } "
@@ -181,6 +188,7 @@ Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
     if (own_stream_) (void)hipStreamSynchronize(own_stream_);
     (void)hipFree(ws_);
+    (void)hipFree(small_mem_);
     (void)hipFree(d_gear_);
     (void)hipFree(d_data_);
     (void)hipFree(d_out_);
@@ -334,6 +342,12 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     }
     int rc = ensure_host_staging(n);
     if (rc) return rc;
+    if (algo_ == CDC_ALGO_FASTCDC && n == 1 && !small_skip_ && small_ok(lens[0])) {
+        rc = run_small(d_streams[0], lens[0], d_out, out_cap, first, s);
+        if (rc == CDC_OK) return (int64_t)first[1];
+        if (rc < 0) return rc;
+        // (kSmallFallback: the regular pipeline below)
+    }
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
     uint64_t *h_tails = h + 3 * h_stage_streams_;
@@ -419,13 +433,13 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     // The resolve's last block writes the done word into coherent pinned
     // memory after a system-scope fence: spin on it (wakes faster than a
     // blocking stream sync) for about the batch's expected device time
-    // (bytes at ~2 TB/s, 0.1-5 ms), pausing between polls, then the stream
-    // sync confirms.  Long batches or a busy caller stream fall through to
-    // the blocking sync instead of burning a core.
+    // (bytes at ~2 TB/s, 0.1-2 ms), pausing between polls, then the stream
+    // sync confirms (at most 2 ms of spinning).  Long batches or a busy
+    // caller stream fall through to the blocking sync instead of burning a core.
     {
         const volatile uint64_t *done = h_misc + p3::kStatDone;
         const auto budget = std::chrono::microseconds(
-            std::min<uint64_t>(5000, std::max<uint64_t>(100, timing_.bytes / 2000000)));
+            std::min<uint64_t>(2000, std::max<uint64_t>(100, timing_.bytes / 2000000)));
         const auto t_spin = std::chrono::steady_clock::now();
         while (*done == ~0ull && std::chrono::steady_clock::now() - t_spin < budget) __builtin_ia32_pause();
     }
@@ -461,6 +475,67 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
     timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk];
     timing_.walk_fallback_steps = h_misc[p3::kStatOnDemand];
+    return CDC_OK;
+}
+
+bool Engine::small_ok(uint64_t len) const {
+    // ~len / 2^pmin records expected: keep well inside the kernel's record budget
+    return small_on_ && len > 0 && len <= small::kMaxBytes && (len >> small_pmin_) <= small::kRecCap * 5 / 8;
+}
+
+int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, size_t out_cap, uint64_t *first,
+                      hipStream_t s, bool host_input) {
+    if (!small_mem_) {
+        HIP_TRY(hipMalloc(&small_mem_, small::scratch_bytes() + small::copy_bytes()));
+        HIP_TRY(hipMemset(small_mem_, 0, small::scratch_bytes()));  // the ticket starts at 0
+        uint32_t *b = static_cast<uint32_t *>(small_mem_);
+        small_ws_.brec = reinterpret_cast<uint64_t *>(b);
+        small_ws_.bcnt = b + 2 * small::kMaxBlocks * small::kBlockRecCap;
+        small_ws_.ticket = small_ws_.bcnt + small::kMaxBlocks;
+        small_ws_.stamp = reinterpret_cast<uint64_t *>(static_cast<char *>(small_mem_) + small::scratch_bytes() - 64);
+        small_ws_.copy = static_cast<uint8_t *>(small_mem_) + small::scratch_bytes();
+    }
+    uint64_t *h = static_cast<uint64_t *>(h_stage_);
+    uint64_t *h_misc = h + 4 * h_stage_streams_;  // (the regular path's stats ++ first[] area)
+    uint64_t *h_first = h_misc + p3::kStatWords;
+    volatile uint64_t *done = h_misc + small::kWordDone;
+    *done = 0;
+    HIP_TRY(small::launch_small(data, len, fp_, d_gear_, small_ws_, d_out, out_cap, h_misc, h_first, host_input, s));
+    ++small_calls_;
+    // The last block writes the done word after a system-scope release: spin on
+    // it (a call is ~20-60 us of device time), then the stream sync confirms.
+    const auto t_spin = std::chrono::steady_clock::now();
+    while (*done == 0 && std::chrono::steady_clock::now() - t_spin < std::chrono::microseconds(2000))
+        __builtin_ia32_pause();
+    if (*done == 0) HIP_TRY(hipStreamSynchronize(s));
+    if (*done != 1) {
+        set_error("small FastCDC kernel did not report back");
+        return CDC_EDEVICE;
+    }
+    timing_pending_ = false;
+    timing_.candidates = h_misc[small::kWordRecords];
+    timing_.overflow_spans = 0;
+    timing_.fixup_iterations = 0;
+    timing_.walk_fallback_steps = 0;
+    if (fp_.diag & small::kDiagStamps) {
+        const uint64_t *t = h_misc + small::kWordStamp0;
+        std::fprintf(stderr, "small: %llu B, us from block 0's start: last block %.2f, records %.2f, links %.2f "
+                             "(%llu rounds), walk %.2f, output %.2f\n",
+                     (unsigned long long)len, (t[1] - t[0]) / 100.0, (t[2] - t[0]) / 100.0, (t[3] - t[0]) / 100.0,
+                     (unsigned long long)t[7], (t[4] - t[0]) / 100.0, (t[5] - t[0]) / 100.0);
+        std::fprintf(stderr, "  round 0 max cycles per lane: load+trunc %llu, link %llu, successor %llu; rounds end at",
+                     (unsigned long long)(t[6] & 0x1FFFFF), (unsigned long long)((t[6] >> 21) & 0x1FFFFF),
+                     (unsigned long long)(t[6] >> 42));
+        for (int k = 0; k < 4; ++k)
+            if (h_first[2 + k]) std::fprintf(stderr, " %.2f", (h_first[2 + k] - t[0]) / 100.0);
+        std::fprintf(stderr, "\n");
+    }
+    if (h_misc[small::kWordFallback]) {
+        ++small_fallbacks_;
+        return kSmallFallback;
+    }
+    first[0] = 0;
+    first[1] = h_first[1];
     return CDC_OK;
 }
 
@@ -528,6 +603,7 @@ int64_t Engine::fs_write(const uint8_t *data, size_t len, size_t seg_size, std::
     // ChunkStorage::write (storage.rs:84-100): StorageWriter::write per
     // seg_size slice, then flush -- through the streaming write path.
     int rc = write_begin();
+    if (rc) return rc;  // (e.g. a streaming write in progress: left alone)
     for (size_t off = 0; !rc && off < len; off += seg_size)
         rc = write_segment(data + off, std::min(seg_size, len - off));
     if (rc) {
@@ -670,7 +746,7 @@ int Engine::init_walk(const uint32_t *seq) {
     wp.avg = avg_;
     wp.max = max_;
     wp.rabin_mask = (1ull << cdc_log2_round(avg_)) - 1;
-    wp.rabin_shift = (uint32_t)(63 - __builtin_clzll(CDC_RABIN_POLY)) - 8;
+
     const uint64_t lspan = avg_ > min_ ? (uint64_t)(avg_ - min_) : 1;
     const uint32_t lb = cdc_log2_round(lspan);
     wp.leap_thr = CDC_LEAP_THRESHOLD[lb > 32 ? 32 : lb];
@@ -767,10 +843,15 @@ int Engine::init_walk(const uint32_t *seq) {
     wp.seg_words = (uint32_t)((1ull << seg_log2_) / 64);
     wp.piece_log2 = seg_log2_ < 15 ? seg_log2_ : 15;  // data-parallel passes: 32 KiB pieces
     wp.bm = nullptr;
-    // Tables: Rabin mod/out (appending a byte; sliding one out of the window),
-    // LeapCDC window-hash table.
+    HIP_TRY(hipMalloc(&d_wtabs_, 768 * sizeof(uint64_t)));
+    wp.tabs = d_wtabs_;
+    return load_walk_tables(CDC_RABIN_POLY);
+}
+
+// Tables: Rabin mod/out of polynomial P (appending a byte; sliding one out of
+// the window), LeapCDC window-hash table; and the digest's top-byte shift.
+int Engine::load_walk_tables(uint64_t P) {
     uint64_t t[768];
-    const uint64_t P = CDC_RABIN_POLY;
     const int deg = 63 - __builtin_clzll(P);
     for (uint64_t b = 0; b < 256; ++b) {
         t[b] = gf2_mod(b << deg, P) | (b << deg);
@@ -779,10 +860,31 @@ int Engine::init_walk(const uint32_t *seq) {
         t[256 + b] = h;
         t[512 + b] = splitmix_word(CDC_LEAP_SEED + (b + 1) * 0x9E3779B97F4A7C15ull);
     }
-    HIP_TRY(hipMalloc(&d_wtabs_, sizeof t));
+    HIP_TRY(hipSetDevice(device_));
     HIP_TRY(hipMemcpy(d_wtabs_, t, sizeof t, hipMemcpyHostToDevice));
-    wp.tabs = d_wtabs_;
+    wp_.rabin_shift = (uint32_t)deg - 8;
     return CDC_OK;
+}
+
+int Engine::set_rabin_poly(uint64_t P) {
+    if (algo_ != CDC_ALGO_RABIN) {
+        set_error("cdc_set_rabin_poly: not a RabinChunker handle");
+        return CDC_EINVAL;
+    }
+    const int deg = P ? 63 - __builtin_clzll(P) : -1;
+    if (deg < 9 || deg > 56) {
+        set_error("cdc_set_rabin_poly: polynomial degree must be 9..56");
+        return CDC_EINVAL;
+    }
+    HIP_TRY(hipSetDevice(device_));
+    HIP_TRY(hipStreamSynchronize(own_stream_));
+    // The degree decides the bitmap kernel and whether it writes the quiet-run
+    // summary (walk::bits_write_summary): the workspace is laid out again.
+    (void)hipFree(wws_);
+    wws_ = nullptr;
+    wws_segs_ = 0;
+    wws_streams_ = 0;
+    return load_walk_tables(P);
 }
 
 int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {

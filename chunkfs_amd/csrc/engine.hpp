@@ -18,18 +18,21 @@
 #include "../../include/chunkfs_amd.h"
 #include "cdc_kernels.hpp"
 #include "fastcdc.hpp"
+#include "small.hpp"
 #include "walk.hpp"
 
 namespace cdc {
 
 // Pageable -> pinned copies of the host path split over a few threads (one
-// core copies ~20 GB/s, below what the H2D DMA takes).  Helpers spin briefly
-// after a job (the next 1 MiB segment usually follows within microseconds),
-// then sleep.  copy() returns when every part is done (hostpath.cpp).
+// core copies ~20 GB/s, below what the H2D DMA takes).  One pool per process
+// (CopyPool::shared), helpers spin briefly after a job (the next 1 MiB segment
+// usually follows within microseconds), then sleep.  copy() returns when
+// every part is done (hostpath.cpp).
 class CopyPool {
   public:
-    explicit CopyPool(unsigned threads);
+    CopyPool(unsigned threads, unsigned spin_us);
     ~CopyPool();
+    static CopyPool &shared();
     void copy(void *dst, const void *src, size_t n);
     unsigned threads() const { return (unsigned)th_.size() + 1; }
 
@@ -37,8 +40,9 @@ class CopyPool {
     void run(unsigned id);
     void part(unsigned id, unsigned parts);
     std::vector<std::thread> th_;
-    std::mutex m_;
+    std::mutex m_, job_m_;
     std::condition_variable cv_;
+    unsigned spin_us_ = 200;
     std::atomic<uint64_t> gen_{0};
     std::atomic<unsigned> left_{0};
     std::atomic<bool> stop_{false};
@@ -73,6 +77,7 @@ class Engine {
     int write_begin();
     int write_segment(const uint8_t *data, size_t len);
     int64_t write_finish(std::vector<uint64_t> &spans, double *seconds);
+    int64_t write_drain(uint64_t *out, size_t cap);
     // Host-path statistics: calls, upload s, total s of chunk_host; chunking s
     // and segments of the current / last streaming write.
     int host_stats(double *v, size_t n) const;
@@ -89,6 +94,7 @@ class Engine {
     size_t max_chunks(size_t len) const { return len / min_chunk() + 1; }
     size_t batch_max_chunks(size_t n, const uint64_t *lens) const;
     int set_gear(const uint64_t *gear);
+    int set_rabin_poly(uint64_t poly);
     const char *describe() const { return describe_.c_str(); }
     // Kernel durations of the last batch: a FastCDC batch whose done word was
     // seen returns before its kernels retire, and its events are read here,
@@ -116,11 +122,18 @@ class Engine {
     int ensure_host_staging(size_t n);
     int run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
                  uint64_t *first, hipStream_t s);
+    // One small FastCDC stream in one launch (small.hip): CDC_OK, kSmallFallback
+    // (a budget was exceeded: run the regular pipeline) or a CDC_E* code.
+    static constexpr int kSmallFallback = 1;
+    bool small_ok(uint64_t len) const;
+    int run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, size_t out_cap, uint64_t *first,
+                  hipStream_t s, bool host_input = false);
     int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                   cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
     // Rabin / Ultra / Leap / Seq: the segment-walk engine (walk.hip).
     bool is_walk() const { return algo_ != CDC_ALGO_FASTCDC && algo_ != CDC_ALGO_FIXED; }
     int init_walk(const uint32_t *seq);
+    int load_walk_tables(uint64_t rabin_poly);
     int ensure_walk_workspace(uint64_t segs, size_t n);
     int run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64_t *first, hipStream_t s);
     // Host boundary (hostpath.cpp).
@@ -186,7 +199,8 @@ class Engine {
     static constexpr size_t kWriteWindow = size_t(256) << 20;
     static constexpr size_t kRingDirect = size_t(16) << 20;  // chunk_data above this: pageable hipMemcpyAsync
     void *h_ring_ = nullptr;
-    std::unique_ptr<CopyPool> pool_;
+    uint8_t *h_ring_dev_ = nullptr;  // the ring as the device addresses it (small-path kernel reads)
+    CopyPool *pool_ = nullptr;  // CopyPool::shared()
     hipEvent_t ring_ev_[kRingSlots] = {};
     uint32_t ring_next_ = 0;
     hipStream_t copy_stream_ = nullptr;
@@ -195,8 +209,9 @@ class Engine {
     size_t h_out_cap_ = 0;
     uint8_t *ws_win_[2] = {nullptr, nullptr};
     struct WriteState {
-        bool active = false;
+        bool active = false, failed = false;
         int cur = 0;
+        size_t drained = 0;  // spans already returned by cdc_write_drain
         size_t reserve = 0, carry = 0, fill = 0;
         uint64_t bytes = 0, segments = 0;
         double t0 = 0, chunk_s = 0;
@@ -221,6 +236,14 @@ class Engine {
     // they were uploaded into.
     std::vector<uint64_t> tables_;
     uint64_t ws_gen_ = 0, tables_gen_ = ~0ull;
+    // Small-stream path (small.hip): on unless CHUNKFS_AMD_SMALL=0; its input
+    // straight from the pinned ring slot (no H2D copy) unless CHUNKFS_AMD_SMALL_ZC=0.
+    bool small_on_ = false, small_zc_ = true;
+    uint32_t small_pmin_ = 0;  // min(popcount mask_s, popcount mask_l): records ~ 2^-pmin per byte
+    bool small_skip_ = false;  // chunk_host's fallback call: the kernel already declined the bytes
+    void *small_mem_ = nullptr;
+    small::Scratch small_ws_{};
+    uint64_t small_calls_ = 0, small_fallbacks_ = 0;
     uint64_t last_spans_ = 0;  // spans of the last FastCDC batch (debug_copy)
     uint64_t out_cap_ = 0;     // capacity of the current batch's output (resolve bound)
 

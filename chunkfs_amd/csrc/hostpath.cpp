@@ -48,8 +48,23 @@ double now_s() {
 
 // ---- copy pool ----------------------------------------------------------------
 
-CopyPool::CopyPool(unsigned threads) {
+CopyPool::CopyPool(unsigned threads, unsigned spin_us) : spin_us_(spin_us) {
     for (unsigned i = 1; i < threads; ++i) th_.emplace_back([this, i] { run(i); });
+}
+
+// One pool per process, shared by every handle (helpers are capped at 16
+// threads whatever the number of handles): CHUNKFS_AMD_COPY_THREADS threads
+// (default 4, the caller's included), helpers spinning CHUNKFS_AMD_COPY_SPIN_US
+// microseconds (default 200) for the next job before they sleep.
+CopyPool &CopyPool::shared() {
+    static CopyPool pool([] {
+        const char *e = std::getenv("CHUNKFS_AMD_COPY_THREADS");
+        return (unsigned)std::max(1, std::min(e ? std::atoi(e) : 4, 16));
+    }(), [] {
+        const char *e = std::getenv("CHUNKFS_AMD_COPY_SPIN_US");
+        return (unsigned)std::max(0, std::min(e ? std::atoi(e) : 200, 100000));
+    }());
+    return pool;
 }
 
 CopyPool::~CopyPool() {
@@ -71,12 +86,13 @@ void CopyPool::part(unsigned id, unsigned parts) {
 void CopyPool::run(unsigned id) {
     uint64_t seen = 0;
     for (;;) {
-        // spin ~1 ms for the next job (a streaming write hands over a segment
-        // every ~50 us; a sleeping helper takes ~100 us to wake), then sleep
+        // spin briefly for the next job (a streaming write hands over a
+        // segment every ~50 us; a sleeping helper takes ~100 us to wake), then
+        // sleep
         const auto t0 = std::chrono::steady_clock::now();
         uint64_t g = gen_.load(std::memory_order_acquire);
         while (g == seen && !stop_.load(std::memory_order_relaxed) &&
-               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(1000)) {
+               std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(spin_us_)) {
             __builtin_ia32_pause();
             g = gen_.load(std::memory_order_acquire);
         }
@@ -98,6 +114,7 @@ void CopyPool::copy(void *dst, const void *src, size_t n) {
         std::memcpy(dst, src, n);
         return;
     }
+    std::lock_guard<std::mutex> job(job_m_);  // one job at a time (handles on several threads share the pool)
     dst_ = static_cast<uint8_t *>(dst);
     src_ = static_cast<const uint8_t *>(src);
     n_ = n;
@@ -116,13 +133,9 @@ void CopyPool::copy(void *dst, const void *src, size_t n) {
 
 int Engine::ensure_ring() {
     if (h_ring_) return CDC_OK;
-    if (!pool_) {
-        // CHUNKFS_AMD_COPY_THREADS: threads of the pageable -> pinned copy (default 4)
-        const char *e = std::getenv("CHUNKFS_AMD_COPY_THREADS");
-        const int t = e ? std::atoi(e) : 4;
-        pool_ = std::make_unique<CopyPool>((unsigned)std::max(1, std::min(t, 16)));
-    }
+    if (!pool_) pool_ = &CopyPool::shared();
     HIP_TRY(hipHostMalloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocDefault));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_ring_dev_), h_ring_, 0));
     for (auto &e : ring_ev_) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&copy_done_, hipEventDisableTiming));
@@ -187,12 +200,38 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
     const size_t need = max_chunks(len);
     if (!rc) rc = ensure_host_out(need);
     if (rc) return rc;
+    int64_t count = -1;
+    double t1 = t0;
+    bool small_tried = false;
+    // FastCDC calls of the reference's size (StorageWriter's 1 MiB segments +
+    // the carried chunk): the bytes go into a pinned ring slot and the one-
+    // launch small kernel reads them there over PCIe -- no DMA, no second
+    // kernel on the call's critical path (small.hip).  A call the kernel's
+    // budgets cannot take falls through to the regular upload + pipeline.
+    if (algo_ == CDC_ALGO_FASTCDC && small_zc_ && !digests && small_ok(len) && len <= kRingSlot) {
+        rc = ensure_host_staging(1);
+        if (rc) return rc;
+        const uint32_t k = ring_next_;
+        ring_next_ = (ring_next_ + 1) % kRingSlots;
+        HIP_TRY(hipEventSynchronize(ring_ev_[k]));
+        uint8_t *slot = static_cast<uint8_t *>(h_ring_) + (size_t)k * kRingSlot;
+        pool_->copy(slot, data, len);
+        t1 = now_s();
+        uint64_t first[2] = {0, 0};
+        rc = run_small(h_ring_dev_ + (size_t)k * kRingSlot, len, d_hout_, need, first, own_stream_, true);
+        HIP_TRY(hipEventRecord(ring_ev_[k], own_stream_));  // the slot is free once the kernel retires
+        if (rc < 0) return rc;
+        if (rc == CDC_OK) count = (int64_t)first[1];
+        small_tried = true;
+    }
     // Small calls (the reference's 1 MiB segments) go through the pinned ring
     // in 256 KiB pieces, so that the CPU copy of one piece overlaps the DMA of
     // the previous one; large buffers take HIP's own pageable path, which
     // stages with several threads (measured 51 vs 31 GiB/s for the single-
     // thread ring on 1 GiB).
-    if (len <= kRingDirect) {
+    if (count >= 0) {
+        // (chunked by the small kernel from the ring slot)
+    } else if (len <= kRingDirect) {
         // (4 MiB pieces, each copied by the pool and moved by one DMA: one
         // 1 MiB call is one hand-off and one hipMemcpyAsync)
         rc = upload(data, len, d_data_, own_stream_, kRingSlot);
@@ -200,13 +239,16 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
     } else {
         HIP_TRY(hipMemcpyAsync(d_data_, data, len, hipMemcpyHostToDevice, own_stream_));
     }
-    const double t1 = now_s();
-    const uint8_t *p = d_data_;
-    const uint64_t l = len;
-    uint64_t first[2] = {0, 0};
-    const int64_t count = chunk_batch_device(1, &p, &l, reinterpret_cast<cdc_chunk_t *>(d_hout_), need, first,
-                                             own_stream_);
-    if (count < 0) return count;
+    if (count < 0) {
+        t1 = now_s();
+        const uint8_t *p = d_data_;
+        const uint64_t l = len;
+        uint64_t first[2] = {0, 0};
+        small_skip_ = small_tried;  // (the small kernel already declined these bytes)
+        count = chunk_batch_device(1, &p, &l, reinterpret_cast<cdc_chunk_t *>(d_hout_), need, first, own_stream_);
+        small_skip_ = false;
+        if (count < 0) return count;
+    }
     const size_t copy = (size_t)count < cap ? (size_t)count : cap;
     if (digests && copy) {
         if (d_out_cap_ < (size_t)count) {  // the SHA-256 kernel reads the chunk list from HBM
@@ -242,6 +284,10 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
 
 int Engine::write_begin() {
     HIP_TRY(hipSetDevice(device_));
+    if (wr_.active) {  // (never silently drop a write in progress)
+        set_error("cdc_write_begin: a write is already in progress on this handle (cdc_write_finish ends it)");
+        return CDC_EINVAL;
+    }
     int rc = ensure_ring();
     if (rc) return rc;
     // A window holds the carried chunk (<= max bytes) at offset 0, then the
@@ -306,20 +352,36 @@ int Engine::write_segment(const uint8_t *data, size_t len) {
         set_error("cdc_write_segment: no write in progress (cdc_write_begin)");
         return CDC_EINVAL;
     }
+    if (wr_.failed) {
+        set_error("cdc_write_segment: an earlier call of this write failed (cdc_write_finish ends it)");
+        return CDC_EINVAL;
+    }
     if (len && !data) {
         set_error("cdc_write_segment: data is NULL");
         return CDC_EINVAL;
     }
-    HIP_TRY(hipSetDevice(device_));
+    // Any failure past this point leaves the window state unknown: the write
+    // is marked failed and cdc_write_finish reports an error, never spans.
+    if (hipSetDevice(device_) != hipSuccess) {
+        wr_.failed = true;
+        set_error("cdc_write_segment: hipSetDevice failed");
+        return CDC_EDEVICE;
+    }
     WriteState &W = wr_;
     while (len) {
         if (W.fill == kWriteWindow) {
             const int rc = write_window(false);
-            if (rc) return rc;
+            if (rc) {
+                W.failed = true;
+                return rc;
+            }
         }
         const size_t n = std::min(len, kWriteWindow - W.fill);
         const int rc = upload(data, n, ws_win_[W.cur] + W.carry + W.fill, copy_stream_, kRingSlot);
-        if (rc) return rc;
+        if (rc) {
+            W.failed = true;
+            return rc;
+        }
         W.fill += n;
         W.bytes += n;
         data += n;
@@ -334,19 +396,42 @@ int64_t Engine::write_finish(std::vector<uint64_t> &spans, double *seconds) {
         set_error("cdc_write_finish: no write in progress (cdc_write_begin)");
         return CDC_EINVAL;
     }
+    wr_.active = false;
+    if (wr_.failed) {
+        set_error("cdc_write_finish: a cdc_write_segment of this write failed; its spans are unknown");
+        return CDC_EDEVICE;
+    }
     HIP_TRY(hipSetDevice(device_));
     const int rc = write_window(true);  // StorageWriter::flush: the rest is the last span
-    wr_.active = false;
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(copy_stream_));
-    spans.swap(wr_.spans);
+    spans.assign(wr_.spans.begin() + (ptrdiff_t)wr_.drained, wr_.spans.end());
     if (seconds) *seconds = now_s() - wr_.t0;
     return (int64_t)spans.size();
 }
 
+// Spans final so far (file order), oldest first, that no drain has returned:
+// every chunk of a chunked device window but its last.  The caller may
+// release the bytes those spans cover.
+int64_t Engine::write_drain(uint64_t *out, size_t cap) {
+    if (!wr_.active) {
+        set_error("cdc_write_drain: no write in progress (cdc_write_begin)");
+        return CDC_EINVAL;
+    }
+    if (cap && !out) {
+        set_error("cdc_write_drain: span_lengths is NULL");
+        return CDC_EINVAL;
+    }
+    const size_t k = std::min(cap, wr_.spans.size() - wr_.drained);
+    std::memcpy(out, wr_.spans.data() + wr_.drained, k * sizeof(uint64_t));
+    wr_.drained += k;
+    return (int64_t)k;
+}
+
 int Engine::host_stats(double *v, size_t n) const {
-    const double s[5] = {(double)host_.calls, host_.upload_s, host_.total_s, wr_.chunk_s, (double)wr_.segments};
-    for (size_t i = 0; i < n && i < 5; ++i) v[i] = s[i];
+    const double s[7] = {(double)host_.calls, host_.upload_s, host_.total_s, wr_.chunk_s, (double)wr_.segments,
+                         (double)small_calls_, (double)small_fallbacks_};
+    for (size_t i = 0; i < n && i < 7; ++i) v[i] = s[i];
     return CDC_OK;
 }
 

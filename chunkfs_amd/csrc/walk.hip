@@ -664,8 +664,8 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
 
 // A fix-up round runs only while the previous one changed exits and those
 // were not mostly quiet-run re-walks (the host applies the same rule and hands
-// a quiet-dominated stream to the in-order pass; WalkState::flags[3] counts
-// quiet re-walks in its high half).
+// a quiet-dominated stream to the in-order pass; WalkState::flags[3] counts,
+// in its high half, the chains of flags[0] whose changed exit was a quiet run).
 __device__ __forceinline__ bool round_stops(const unsigned long long *gate) {
     return gate && (gate[0] == 0 || 2 * (gate[3] >> 32) >= gate[0]);
 }
@@ -1515,15 +1515,19 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
         uint64_t xo;
         bool qr;
         const bool changed = wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, lane, xo, qr);
-        // (quiet re-walks counted in the high half: the host hands rounds of
-        // mostly phase-locked quiet segments to the in-order pass early)
-        if (qr && changed && lane == 0) atomicAdd(&ws.flags[3], 1ull << 32);
         if (!changed) break;
         if (seg_end >= len) break;  // the stream's last segment: no successor
         if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
             if (lane == 0) {
                 atomicAdd(&ws.flags[0], 1ull);  // a successor needs another round
                 atomicMin(&ws.flags[2], (unsigned long long)gg);
+                // Of those, the chains whose changed exit came out of a quiet
+                // run (high half; the same count as flags[0], restricted): the
+                // host hands rounds of mostly phase-locked quiet segments to
+                // the in-order pass early.  Run-ahead steps inside one chain
+                // are not counted, so scattered small quiet islands in random
+                // data do not trip the hand-off.
+                if (qr) atomicAdd(&ws.flags[3], 1ull << 32);
             }
             break;
         }

@@ -116,6 +116,14 @@ const char *cdc_last_error(void);
  * maintainer pins parity with the Rust crate by passing the crate's table. */
 int cdc_set_gear(cdc_handle_t *h, const uint64_t gear[256]);
 
+/* Install the Rabin polynomial of a CDC_ALGO_RABIN handle (the reference's
+ * RabinChunker carries its ChunkerParams tables, rabin.rs:34-51; the crate's
+ * polynomial is absent offline, include/chunkfs_amd_cdc_params.h holds a
+ * stand-in).  Degree 9..56 (the 48-byte window digest shifted by a byte stays
+ * inside 64 bits); the tables are rebuilt for the handle.  CDC_EINVAL for
+ * another algorithm or degree. */
+int cdc_set_rabin_poly(cdc_handle_t *h, uint64_t poly);
+
 /* ---- Device-resident batch API (configs 2, 4, 5: inputs already in HBM) --
  * Chunk n independent streams in one pass.  d_streams[i] are DEVICE pointers
  * (16-byte aligned), lens[i] their byte lengths (host arrays of n entries).
@@ -181,11 +189,23 @@ int64_t cdc_fs_write(cdc_handle_t *h, const uint8_t *data, size_t len,
  * ring and uploaded asynchronously while the caller goes on; the device
  * chunks 256 MiB windows of the file, carrying each window's last chunk to the
  * next one in HBM.  The caller's bytes are not retained after a call returns.
- * One write per handle at a time. */
+ * One write per handle at a time: cdc_write_begin on a handle whose write is
+ * in progress returns CDC_EINVAL.  A failing cdc_write_segment marks the write
+ * failed: later segments return CDC_EINVAL and cdc_write_finish returns an
+ * error (never spans of unknown correctness) and ends the write. */
 int cdc_write_begin(cdc_handle_t *h);
 int cdc_write_segment(cdc_handle_t *h, const uint8_t *data, size_t len);
-/* Span lengths (min(count, cap) written), returns the span count; *seconds
- * (may be NULL) = wall time since cdc_write_begin. */
+/* Spans that became final since the last drain, oldest first: moves
+ * min(pending, cap) of them into span_lengths and returns how many it moved
+ * (0: none pending).  Spans become final each time a device window has been
+ * chunked, i.e. every 256 MiB of uploaded bytes, so a caller that hashes and
+ * stores each span as StorageWriter::write does (storage.rs:324-350) needs to
+ * keep only the bytes from the end of the last drained span on: at most one
+ * window (256 MiB) + the segment in hand + max bytes, as the reference's
+ * write_from_stream keeps SEG_SIZE + max. */
+int64_t cdc_write_drain(cdc_handle_t *h, uint64_t *span_lengths, size_t cap);
+/* The spans no cdc_write_drain returned (min(count, cap) written), returns
+ * their count; *seconds (may be NULL) = wall time since cdc_write_begin. */
 int64_t cdc_write_finish(cdc_handle_t *h, uint64_t *span_lengths, size_t cap,
                          double *seconds);
 

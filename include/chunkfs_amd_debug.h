@@ -27,7 +27,9 @@ int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes);
 /* Host-path statistics into v[0..n): cdc_chunk_data calls, their upload
  * seconds (CPU copy into the pinned ring + queueing the H2D), their total
  * seconds, then the chunking seconds and segment count of the current or
- * last streaming write (cdc_write_*). */
+ * last streaming write (cdc_write_*), then the FastCDC batches taken by the
+ * one-launch small-stream kernel (small.hip) and how many of them fell back
+ * to the regular pipeline (a record / start budget exceeded). */
 int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n);
 /* Kernel times of the FastCDC batch `back` calls before the last one (0 = the
  * last; up to 63 back): scan_ms, resolve_ms, total_ms of t (the other fields

@@ -270,9 +270,10 @@ static uint64_t pol_mod(uint64_t x, uint64_t p)
     return x;
 }
 
-static void rabin_tables(uint64_t mod_t[256], uint64_t out_t[256])
+/* Tables of polynomial P (RabinChunker's ChunkerParams, rabin.rs:38; the
+ * built-in CDC_RABIN_POLY unless a caller passes another one). */
+static void rabin_tables_p(uint64_t P, uint64_t mod_t[256], uint64_t out_t[256])
 {
-    const uint64_t P = CDC_RABIN_POLY;
     const int deg = 63 - __builtin_clzll(P);
     for (uint64_t b = 0; b < 256; b++) {
         mod_t[b] = pol_mod(b << deg, P) | (b << deg);
@@ -282,14 +283,19 @@ static void rabin_tables(uint64_t mod_t[256], uint64_t out_t[256])
     }
 }
 
+static void rabin_tables(uint64_t mod_t[256], uint64_t out_t[256]) { rabin_tables_p(CDC_RABIN_POLY, mod_t, out_t); }
+
+/* Degrees a Rabin polynomial may have here: the digest shifted left by 8
+ * stays inside 64 bits, and the top byte index (deg - 8) is >= 1. */
+int oracle_rabin_poly_ok(uint64_t P) { return P && (63 - __builtin_clzll(P)) >= 9 && (63 - __builtin_clzll(P)) <= 56; }
+
 static uint64_t cut_rabin(const uint8_t *src, uint64_t n, uint32_t min, uint32_t max, uint64_t mask,
-                          const uint64_t *mod_t, const uint64_t *out_t)
+                          const uint64_t *mod_t, const uint64_t *out_t, int shift)
 {
     if (n <= min) return n;
     const uint64_t end = n < max ? n : max;
     const uint64_t W = CDC_RABIN_WINDOW;
     const uint64_t start = min >= W ? min - W : 0;
-    const int shift = (63 - __builtin_clzll(CDC_RABIN_POLY)) - 8;
     uint64_t d = 0;
     for (uint64_t i = start; i < end; i++) {
         d ^= out_t[i >= start + W ? src[i - W] : 0];
@@ -416,18 +422,37 @@ int oracle_cdc_check(int algo, uint32_t min, uint32_t avg, uint32_t max)
 /* chunk_data for algo 2 (Rabin), 4 (Ultra), 5 (Leap), 6 (Seq; seqcfg =
  * {mode (0 increasing, 1 decreasing), seq_length, jump_trigger, jump_size},
  * NULL = defaults).  Same output convention as oracle_fastcdc_chunk. */
+int64_t oracle_cdc_chunk_p(int algo, const uint8_t *data, uint64_t len, uint32_t min, uint32_t avg,
+                           uint32_t max, const uint32_t *seqcfg, uint64_t rabin_poly, uint64_t *offsets,
+                           uint64_t *lengths, uint64_t cap);
+
 int64_t oracle_cdc_chunk(int algo, const uint8_t *data, uint64_t len, uint32_t min, uint32_t avg,
                          uint32_t max, const uint32_t *seqcfg, uint64_t *offsets, uint64_t *lengths,
                          uint64_t cap)
 {
+    return oracle_cdc_chunk_p(algo, data, len, min, avg, max, seqcfg, 0, offsets, lengths, cap);
+}
+
+/* oracle_cdc_chunk with a Rabin polynomial (0 = CDC_RABIN_POLY): the
+ * restatement behind cdc_set_rabin_poly. */
+int64_t oracle_cdc_chunk_p(int algo, const uint8_t *data, uint64_t len, uint32_t min, uint32_t avg,
+                           uint32_t max, const uint32_t *seqcfg, uint64_t rabin_poly, uint64_t *offsets,
+                           uint64_t *lengths, uint64_t cap)
+{
     if (oracle_cdc_check(algo, min, avg, max)) return -1;
-    static uint64_t mod_t[256], out_t[256], e[256];
+    const uint64_t P = rabin_poly ? rabin_poly : CDC_RABIN_POLY;
+    if (!oracle_rabin_poly_ok(P)) return -1;
+    static uint64_t mod_t[256], out_t[256], e[256], cur_p = 0;
     static int init = 0;
     if (!init) {
-        rabin_tables(mod_t, out_t);
         leap_table(e);
         init = 1;
     }
+    if (cur_p != P) {
+        rabin_tables_p(P, mod_t, out_t);
+        cur_p = P;
+    }
+    const int rshift = (63 - __builtin_clzll(P)) - 8;
     const uint32_t defcfg[4] = {0, CDC_SEQ_LENGTH, CDC_SEQ_JUMP_TRIGGER, CDC_SEQ_JUMP_SIZE};
     const uint32_t *cfg = seqcfg ? seqcfg : defcfg;
     if (algo == 6 && (cfg[0] > 1 || cfg[1] == 0 || cfg[2] == 0 || cfg[3] == 0)) return -1;
@@ -437,7 +462,7 @@ int64_t oracle_cdc_chunk(int algo, const uint8_t *data, uint64_t len, uint32_t m
     while (processed < len) {
         const uint8_t *s = data + processed;
         const uint64_t n = len - processed;
-        uint64_t cut = algo == 2 ? cut_rabin(s, n, min, max, rmask, mod_t, out_t)
+        uint64_t cut = algo == 2 ? cut_rabin(s, n, min, max, rmask, mod_t, out_t, rshift)
                      : algo == 4 ? cut_ultra(s, n, min, avg, max)
                      : algo == 5 ? cut_leap(s, n, min, max, thr, e)
                                  : cut_seq(s, n, min, max, cfg);

@@ -55,6 +55,10 @@ def lib():
                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, u64p, u64p,
                                        ctypes.c_uint64]
         L.oracle_cdc_chunk.restype = ctypes.c_int64
+        L.oracle_cdc_chunk_p.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                         ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, u64p,
+                                         u64p, ctypes.c_uint64]
+        L.oracle_cdc_chunk_p.restype = ctypes.c_int64
         L.oracle_cdc_check.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_cdc_check.restype = ctypes.c_int
         L.oracle_leap_threshold.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
@@ -118,18 +122,20 @@ def fixed(n, cs):
 ALGOS = {"fast": 0, "fixed": 1, "rabin": 2, "ultra": 4, "leap": 5, "seq": 6}
 
 
-def cdc(algo, data, mn, avg, mx, seqcfg=None):
+def cdc(algo, data, mn, avg, mx, seqcfg=None, rabin_poly=None):
     """(n, 2) uint64 (offset, length) of Rabin / Ultra / Leap / Seq over the whole
     buffer (oracle/cdc_oracle.c; parity unpinned, see the header there).
-    seqcfg = (mode, seq_length, jump_trigger, jump_size) for "seq"."""
+    seqcfg = (mode, seq_length, jump_trigger, jump_size) for "seq"; rabin_poly
+    = a Rabin polynomial other than the built-in one (cdc_set_rabin_poly)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     n = data.size
     cap = n // mn + 2
     off = np.empty(cap, dtype=np.uint64)
     ln = np.empty(cap, dtype=np.uint64)
     cfg = None if seqcfg is None else np.ascontiguousarray(seqcfg, dtype=np.uint32)
-    cnt = lib().oracle_cdc_chunk(ALGOS[algo], _ptr(data), n, mn, avg, mx,
-                                 None if cfg is None else _ptr(cfg), _u64p(off), _u64p(ln), cap)
+    cnt = lib().oracle_cdc_chunk_p(ALGOS[algo], _ptr(data), n, mn, avg, mx,
+                                   None if cfg is None else _ptr(cfg), int(rabin_poly or 0), _u64p(off),
+                                   _u64p(ln), cap)
     if cnt < 0:
         raise ValueError("invalid sizes")
     assert cnt <= cap

@@ -72,14 +72,25 @@ def test_stream_write_matches_storage_writer(algo):
 
 def test_stream_write_crosses_device_windows():
     """600 MiB in 1 MiB segments: the 256 MiB device windows and the carried
-    chunk between them (the reference's `rest`, in HBM here)."""
+    chunk between them (the reference's `rest`, in HBM here).  Spans are
+    drained as windows complete (cdc_write_drain): drains + finish == the
+    whole write, and the first drain comes after the first window."""
     import chunkfs_amd as c
     data = oracle.splitmix64_bytes(600 << 20, 5)
     ch = _chunker("fast")
     w = c.StreamWriter(ch)
+    drained, first_at, covered = [], None, 0
     for off in range(0, data.size, 1 << 20):
         w.write(data[off:off + (1 << 20)])
+        d = w.drain()
+        if d.size and first_at is None:
+            first_at = off + (1 << 20)
+        covered += int(d.sum())
+        assert covered <= off + (1 << 20)  # a drained span lies in uploaded bytes
+        drained.append(d)
     spans, _ = w.finish()
+    spans = np.concatenate(drained + [spans])
+    assert first_at is not None and first_at > (256 << 20)
     ref = _whole("fast", data)
     assert spans.shape == ref.shape and (spans == ref).all()
     st = c.host_stats(ch)
@@ -88,6 +99,53 @@ def test_stream_write_crosses_device_windows():
     spans2, _ = c.write_spans(ch, data[:3 << 20])
     ref2 = _whole("fast", data[:3 << 20])
     assert spans2.shape == ref2.shape and (spans2 == ref2).all()
+    ch.close()
+
+
+@pytest.mark.parametrize("algo", ["ultra", "seq"])
+def test_stream_write_window_carry_walk_rules(algo):
+    """The walk engine across the 256 MiB device windows (a lane-walk and a
+    wave-walk rule): just over two windows of random bytes with a zero-filled
+    region straddling the first window boundary, so a window starts inside a
+    quiet run at a carried chunk."""
+    import chunkfs_amd as c
+    n = (512 << 20) + 77777
+    data = oracle.splitmix64_bytes(n, 31)
+    b = 256 << 20
+    data[b - (3 << 20) + 11:b + (2 << 20) + 5] = 0
+    ch = _chunker(algo)
+    w = c.StreamWriter(ch)
+    drained = []
+    for off in range(0, n, 1 << 20):
+        w.write(data[off:off + (1 << 20)])
+        drained.append(w.drain())
+    spans, _ = w.finish()
+    spans = np.concatenate(drained + [spans])
+    ref = _whole(algo, data)
+    assert spans.shape == ref.shape and (spans == ref).all(), algo
+    ch.close()
+
+
+def test_stream_write_begin_twice_and_failure_rules():
+    """cdc_write_begin on a write in progress is refused (the write in
+    progress is kept); finish ends it; a drain without a write is refused."""
+    import chunkfs_amd as c
+    ch = _chunker("fast")
+    data = oracle.splitmix64_bytes(3 << 20, 8)
+    w = c.StreamWriter(ch)
+    w.write(data[:1 << 20])
+    with pytest.raises(c.CdcError):
+        c.StreamWriter(ch)
+    with pytest.raises(c.CdcError):
+        c.write_spans(ch, data)  # cdc_fs_write also begins a write
+    w.write(data[1 << 20:])
+    spans, _ = w.finish()
+    ref = _whole("fast", data)
+    assert spans.shape == ref.shape and (spans == ref).all()
+    with pytest.raises(c.CdcError):
+        w.drain()
+    spans2, _ = c.write_spans(ch, data)  # the handle is free again
+    assert (spans2 == ref).all()
     ch.close()
 
 

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_two_ranks_on_hip_engine():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
-                        "--dist-backend", "gloo", "--rank-parity", "--workload", "batch", "--batch-streams", "8",
+                        "--rank-parity", "--workload", "batch", "--batch-streams", "8",
                         "--batch-stream-bytes", str(8 << 20), "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
@@ -29,3 +29,31 @@ def test_two_ranks_on_hip_engine():
     assert line["config"]["streams_per_gpu"] == 4
     assert line["parity_all_ranks"] is True
     assert line["value"] > 0
+
+
+def test_two_ranks_default_stream_workload():
+    """The driver's own N>1 command shape (`bench.py --gpus N`, default
+    `--workload stream`, default gloo reductions) with small sizes: `value` is
+    config 2 per GPU (weak), the config-4 leg runs its N>1 branch (rank 0 re-times
+    the whole batch alone: the strong-scaling denominator) and the config-5 leg
+    runs every walk rule at avg 2/8/64 KiB across both ranks, checked against
+    the oracle."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
+                        "--rank-parity", "--stream-bytes", str(64 << 20), "--batch-streams", "8",
+                        "--batch-stream-bytes", str(8 << 20), "--config4-steps", "2", "--config5-streams", "4",
+                        "--config5-stream-bytes", str(32 << 20), "--config5-check", str(8 << 20), "--steps", "2",
+                        "--warmup", "1", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["config"]["workload"].startswith("config2")
+    assert line["parity_all_ranks"] is True and line["value"] > 0
+    c4 = line["config4"]
+    assert c4["streams_per_gpu"] == 4 and c4["parity_vs_oracle"] is True
+    assert c4["strong_scaling_efficiency"] > 0 and c4["n1_value_rank0_alone"] > 0
+    c5 = line["config5"]
+    assert c5["streams_per_gpu"] == 2 and len(c5["lines"]) == 12
+    assert all(v["parity_vs_oracle"] is True for v in c5["lines"].values()), c5["lines"]

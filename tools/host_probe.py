@@ -26,6 +26,7 @@ for n in sizes:
     el = (time.perf_counter() - t0) / reps
     st1 = c.host_stats(ch)
     t = ch.last_timing()
-    print(f"n={n:9d}  {el * 1e6:8.1f} us/call  {n / el / 2**30:6.2f} GiB/s  upload "
-          f"{(st1['upload_s'] - st0['upload_s']) / reps * 1e6:6.1f} us  scan {t['scan_ms'] * 1e3:6.1f} us  "
+    print(f"n={n:9d}  {el * 1e6:8.1f} us/call  {n / el / 2**30:6.2f} GiB/s  small "
+          f"{st1['small_calls'] - st0['small_calls']}/{reps} (fallback {st1['small_fallbacks'] - st0['small_fallbacks']})  upload "
+          f"{(st1['upload_s'] - st0['upload_s']) / reps * 1e6:6.1f} us  in C {(st1['total_s'] - st0['total_s']) / reps * 1e6:6.1f} us  scan {t['scan_ms'] * 1e3:6.1f} us  "
           f"resolve {t['resolve_ms'] * 1e3:6.1f} us  device {t['total_ms'] * 1e3:6.1f} us", flush=True)
