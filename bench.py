@@ -521,7 +521,8 @@ def algo_lines(args, eng, w, steps):
 def lowentropy_walk_lines(args, eng, nbytes=256 << 20):
     """Rabin / UltraCDC / LeapCDC / SeqCDC on low-entropy device streams of
     `nbytes` (zeros; a 61-byte period; random bytes with 1-32 MiB zero-filled
-    regions at unaligned offsets), bench sizes: chains from different
+    regions at unaligned offsets; random bytes with a dozen 64-512 KiB zero
+    islands), bench sizes: chains from different
     starts never merge on such data, so these lines time the fix-up rounds
     and the in-order pass (one wave per stream) that the splitmix64 lines
     never reach.  Device GiB/s, the re-walk statistics and bit-exactness vs
@@ -542,9 +543,15 @@ def lowentropy_walk_lines(args, eng, nbytes=256 << 20):
         ln = int(rng.integers(1 << 20, 32 << 20))
         runs[pos:pos + ln] = 0
         pos += ln + int(rng.integers(1 << 16, 8 << 20))
+    # random bytes with a few small zero islands (64-512 KiB): the fix-up
+    # rounds' quiet hand-off must not fire on such mostly random data
+    isl = torch.from_numpy(oracle.splitmix64_bytes(n, 19)).to(eng.dev)
+    for _ in range(12):
+        a = int(rng.integers(0, n - (1 << 19)))
+        isl[a:a + int(rng.integers(1 << 16, 1 << 19))] = 0
     inputs = {"zeros": torch.zeros(n, dtype=torch.uint8, device=eng.dev),
               "periodic61": period.repeat(-(-n // 61))[:n].contiguous(),
-              "zero_runs": runs}
+              "zero_runs": runs, "zero_islands": isl}
     sizes = cfa.SizeParams(args.min, args.avg, args.max)
     res = {}
     for inp, buf in inputs.items():

@@ -1439,27 +1439,36 @@ __device__ __forceinline__ void item_load(const LinkItem &it, const void *safe, 
     for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(src + 4 * i);
 }
 
+// Branch-free: 12 GEAR lookups issued together per batch (one LDS latency per
+// batch instead of one per 4 bytes), hit bits collected in a mask, the first
+// one wins (the same result as trunc_words).
 __device__ __forceinline__ uint32_t item_trunc(const LinkItem &it, const uint32_t (&w)[13], const FastParams &fp,
                                                const uint64_t *tab) {
     if (!it.act || it.len == 0) return kTruncNone;
     if (it.known != kTruncUnknown) return it.known;  // from the scan's flush
     if (!it.fast) return trunc_call(it.data, it.n, it.c, fp, tab);
     const uint32_t r = (uint32_t)(it.w0 & 3);
-    uint64_t h = 0;
-    uint32_t t = kTruncNone;
+    const uint32_t ns = it.ce > it.a0 ? (uint32_t)min(it.ce - it.a0, (uint64_t)64) : 0u;  // d < ns: mask_s
+    uint64_t h = 0, hits = 0;
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const uint32_t a = __builtin_amdgcn_alignbyte(w[k + 1], w[k], r);
+    for (int k0 = 0; k0 < 12; k0 += 3) {
+        uint64_t g[12];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const uint32_t d = 4 * k + b;
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t a = __builtin_amdgcn_alignbyte(w[k0 + k + 1], w[k0 + k], r);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) g[4 * k + b] = tab[(a >> (8 * b)) & 255];
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            const uint32_t d = 4 * k0 + i;
             if (d >= kTruncMax) break;
-            h = shl1_add(h, tab[(a >> (8 * b)) & 255]);
-            const bool hit = d < it.len && !(h & ((it.a0 + d) < it.ce ? fp.mask_s : fp.mask_l));
-            t = (hit && t == kTruncNone) ? d : t;
+            h = shl1_add(h, g[i]);
+            hits |= (uint64_t)((h & (d < ns ? fp.mask_s : fp.mask_l)) == 0) << d;
         }
     }
-    return t;
+    hits &= it.len >= 64 ? ~0ull : (1ull << it.len) - 1;
+    return hits ? (uint32_t)__builtin_ctzll(hits) : kTruncNone;
 }
 
 // The item's link into W.link/W.lrec; a next start that is neither a record
@@ -1782,12 +1791,20 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
             uint32_t nv = 0, e0 = 0, e1 = nlink;
             bool virt = false;
             for (;;) {
+                // (the next pass's bytes are loaded while this pass evaluates:
+                // one memory latency per round instead of one per pass)
+                LinkItem A = link_item(W, fp, virt, e0 + lane, e1);
+                uint32_t wa[13];
+                item_load(A, gear, wa);
                 for (uint32_t base = e0; base < e1; base += 64) {
-                    const LinkItem A = link_item(W, fp, virt, base + lane, e1);
-                    uint32_t wa[13];
-                    item_load(A, gear, wa);
+                    const LinkItem B2 = link_item(W, fp, virt, base + 64 + lane, e1);
+                    uint32_t wb[13];
+                    item_load(B2, gear, wb);
                     const uint32_t tr = (fp.diag & 4) ? kTruncNone : item_trunc(A, wa, fp, tab);
                     item_link(W, fp, tab, A, tr, sl2, nv);
+                    A = B2;
+#pragma unroll
+                    for (int i = 0; i < 13; ++i) wa[i] = wb[i];
                 }
                 wave_sync_lds();
                 if (!virt) CDC_DIAG_T(4);

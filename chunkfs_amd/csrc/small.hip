@@ -211,15 +211,22 @@ __device__ __forceinline__ uint32_t trunc_eval(const uint32_t (&w)[13], uint64_t
     return hits ? (uint32_t)__builtin_ctzll(hits) : kTruncNone;
 }
 
-__device__ __noinline__ uint32_t trunc_bytes(const uint8_t *data, uint64_t c, const Regime &R, const FastParams &fp,
-                                             const uint64_t *tab) {
-    const uint64_t w0 = c + R.a0;
+// (Out of line, arguments by value: a reference would force the caller's
+// Regime / FastParams into scratch memory.)
+__device__ __noinline__ uint32_t trunc_bytes_at(const uint8_t *data, uint64_t w0, uint32_t len, uint32_t ns,
+                                                uint64_t mask_s, uint64_t mask_l, const uint64_t *tab) {
     uint64_t h = 0;
-    for (uint32_t d = 0; d < (uint32_t)(R.tl - R.a0); ++d) {
+    for (uint32_t d = 0; d < len; ++d) {
         h = (h << 1) + tab[(uint32_t)((g_u8 *)data)[w0 + d] * kCopies];
-        if (!(h & ((R.a0 + d) < R.ce ? fp.mask_s : fp.mask_l))) return d;
+        if (!(h & (d < ns ? mask_s : mask_l))) return d;
     }
     return kTruncNone;
+}
+
+__device__ __forceinline__ uint32_t trunc_bytes(const uint8_t *data, uint64_t c, const Regime &R, const FastParams &fp,
+                                                const uint64_t *tab) {
+    const uint32_t ns = R.ce > R.a0 ? (uint32_t)min(R.ce - R.a0, (uint64_t)64) : 0u;
+    return trunc_bytes_at(data, c + R.a0, (uint32_t)(R.tl - R.a0), ns, fp.mask_s, fp.mask_l, tab);
 }
 
 // Next start after a chunk starting at c whose truncated result is t: the
@@ -258,28 +265,6 @@ __device__ __forceinline__ uint32_t run_len(const uint32_t *rec, uint32_t nrec, 
         if (i < nrec && (uint64_t)(rec[i] & kPosMask) < v + R.re) break;
     }
     return k;
-}
-
-// A record's truncated result and its max-cut successor's (v = c + max in the
-// steady regime; kTruncUnknown otherwise), from the input bytes: computed by
-// the scanning wave that found the record, so that the last block's first
-// link round needs no memory access but LDS.
-__device__ __forceinline__ uint32_t record_trunc(const uint8_t *data, uint64_t n, uint64_t c, const FastParams &fp,
-                                                const uint64_t *tab, uint32_t rep) {
-    if (n - c <= fp.min) return kTruncNone | (kTruncUnknown << 8);  // the tail chunk
-    const Regime R = regime(fp, c, n);
-    const uint64_t v = c + R.rem;
-    const bool spec = R.rem == fp.max && n - v > fp.min;
-    const Regime Rv = regime(fp, spec ? v : c, n);
-    uint32_t wc[13], wv[13];
-    const bool ldc = trunc_words_ok(R, c, n), ldv = spec && trunc_words_ok(Rv, v, n);
-    if (ldc) trunc_load(data, n, c + R.a0, wc);
-    if (ldv) trunc_load(data, n, v + Rv.a0, wv);
-    const uint32_t tc = R.tl <= R.a0 ? kTruncNone : ldc ? trunc_eval(wc, c + R.a0, R, fp, tab, rep)
-                                                        : trunc_bytes(data, c, R, fp, tab);
-    const uint32_t tv = !spec ? kTruncUnknown : Rv.tl <= Rv.a0 ? kTruncNone
-                        : ldv ? trunc_eval(wv, v + Rv.a0, Rv, fp, tab, rep) : trunc_bytes(data, v, Rv, fp, tab);
-    return tc | (tv << 8);
 }
 
 __global__ __launch_bounds__(kThreads, 1) void small_kernel(const uint8_t *__restrict__ data, uint64_t n,
@@ -352,11 +337,11 @@ __global__ __launch_bounds__(kThreads, 1) void small_kernel(const uint8_t *__res
                 }
         }
     }
-    // Truncated results of the records (and of their max-cut successors).
-    uint32_t tinfo[kLaneHits] = {0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t s = 0; s < kLaneHits; ++s)
-        if (s < nh) tinfo[s] = record_trunc(data, n, hits[s] & kPosMask, fp, L.tab, rep);
+    // (The records' truncated results are computed by the last block from the
+    // device copy: loads from the host slot here would put a PCIe round trip
+    // per record on every block's critical path.)
+    const uint32_t tinfo[kLaneHits] = {kTruncUnknown | (kTruncUnknown << 8), kTruncUnknown | (kTruncUnknown << 8),
+                                       kTruncUnknown | (kTruncUnknown << 8), kTruncUnknown | (kTruncUnknown << 8)};
     // Records in position order: lanes of a wave, then the block's waves.
     const bool lane_ovf = nh > kLaneHits;
     const uint32_t c = lane_ovf ? 0u : nh;
@@ -471,6 +456,7 @@ __global__ __launch_bounds__(kThreads, 1) void small_kernel(const uint8_t *__res
         uint32_t e0 = 0, e1 = nrec, round = 0;
         for (; e0 < e1 && round < kRounds; ++round) {
             for (uint32_t e = e0 + tid; e < e1; e += kThreads) {
+                if (Q.enx[e] != kNone && !Q.tent[e]) continue;  // linked when it was added (a head)
                 const uint64_t c = Q.epos[e];
                 if (n - c <= fp.min) {  // the tail chunk: it ends the stream
                     Q.enx[e] = kEnd;

@@ -24,11 +24,27 @@ SIZES = [(4096, 8192, 16384), (8192, 16384, 65536), (2048, 8192, 65536), (512, 2
 _cache = {}
 
 
-def chunker(sizes):
+def chunker(sizes, path="small"):
+    """path "small": single streams up to 4 MiB take the one-launch kernel
+    (small.hip; the default); "pipeline": CHUNKFS_AMD_SMALL=0, every batch
+    takes the scan + resolve pipeline (fastcdc.hip)."""
     import chunkfs_amd as c
-    if sizes not in _cache:
-        _cache[sizes] = c.FastChunker(c.SizeParams(*sizes))
-    return _cache[sizes]
+    key = (sizes, path)
+    if key not in _cache:
+        old = os.environ.get("CHUNKFS_AMD_SMALL")
+        if path == "pipeline":
+            os.environ["CHUNKFS_AMD_SMALL"] = "0"
+        try:
+            _cache[key] = c.FastChunker(c.SizeParams(*sizes))
+        finally:
+            if old is None:
+                os.environ.pop("CHUNKFS_AMD_SMALL", None)
+            else:
+                os.environ["CHUNKFS_AMD_SMALL"] = old
+    return _cache[key]
+
+
+PATHS = ["small", "pipeline"]
 
 
 def assert_same(gpu, ref, what=""):
@@ -42,29 +58,32 @@ def assert_same(gpu, ref, what=""):
                     f"gpu={gpu[i].tolist() if i < len(gpu) else None} ref={ref[i].tolist() if i < len(ref) else None}")
 
 
-def test_golden_vectors_on_gpu():
+@pytest.mark.parametrize("path", PATHS)
+def test_golden_vectors_on_gpu(path):
     with open(os.path.join(GOLDEN, "fastcdc_selfconsistent.json")) as f:
         vecs = json.load(f)["vectors"]
     for v in vecs:
         data = make_input(v["pattern"], v["len"], v["seed"])
         assert hashlib.sha256(data.tobytes()).hexdigest() == v["input_sha256"]
-        got = chunker((v["min"], v["avg"], v["max"])).chunk_array(data)
+        got = chunker((v["min"], v["avg"], v["max"]), path).chunk_array(data)
         assert [int(x) for x in got[:, 1]] == v["lengths"], (v["pattern"], v["len"], v["min"])
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("sizes", SIZES)
 @pytest.mark.parametrize("seed", [1, 2])
-def test_random_streams_bit_exact(sizes, seed):
+def test_random_streams_bit_exact(sizes, seed, path):
     for n in [3 * (1 << 20) + 17 * seed, (1 << 20)]:
         data = oracle.splitmix64_bytes(n, seed * 31 + n)
-        assert_same(chunker(sizes).chunk_array(data), oracle.fastcdc(data, *sizes), f"{sizes} n={n}")
+        assert_same(chunker(sizes, path).chunk_array(data), oracle.fastcdc(data, *sizes), f"{sizes} n={n} {path}")
 
 
-def test_tails_of_every_length():
+@pytest.mark.parametrize("path", PATHS)
+def test_tails_of_every_length(path):
     """Every length 0 .. 2*max+1 around the min/max thresholds (CS-3 edge cases)."""
     sizes = (4096, 8192, 16384)
     base = oracle.splitmix64_bytes(2 * 16384 + 64, 77)
-    c = chunker(sizes)
+    c = chunker(sizes, path)
     lens = list(range(0, 200)) + list(range(4000, 4200)) + list(range(8100, 8300)) + \
         list(range(16300, 16500)) + list(range(2 * 16384 - 100, 2 * 16384 + 2))
     for n in lens:
@@ -75,11 +94,12 @@ def test_tails_of_every_length():
     ("const", 5 << 20, 0), ("const", 3 << 20, 0xFF), ("const", 3 << 20, 0x5A),
     ("periodic", 4 << 20, 61), ("periodic", 4 << 20, 4096), ("periodic", 4 << 20, 1),
     ("lowentropy", 4 << 20, 11), ("lowentropy", 4 << 20, 12)])
-def test_low_entropy_and_overflow_paths(pattern, n, seed):
+@pytest.mark.parametrize("path", PATHS)
+def test_low_entropy_and_overflow_paths(pattern, n, seed, path):
     """Constant / periodic data: candidate lists are empty or overflow (slow exact path)."""
     data = make_input(pattern, n, seed)
     for sizes in [(4096, 8192, 16384), (512, 2048, 16384)]:
-        assert_same(chunker(sizes).chunk_array(data), oracle.fastcdc(data, *sizes), f"{pattern} {sizes}")
+        assert_same(chunker(sizes, path).chunk_array(data), oracle.fastcdc(data, *sizes), f"{pattern} {sizes} {path}")
 
 
 def test_unaligned_host_buffer():
@@ -314,6 +334,7 @@ def test_dma_scan_variant_bit_exact(sizes, monkeypatch):
     ragged multi-stream batch incl. low-entropy data and a multi-span stream."""
     import chunkfs_amd as c
     monkeypatch.setenv("CHUNKFS_AMD_DIAG", "1024")
+    monkeypatch.setenv("CHUNKFS_AMD_SMALL", "0")  # (single streams <= 4 MiB would take small.hip)
     ch = c.FastChunker(c.SizeParams(*sizes))
     streams = [oracle.splitmix64_bytes(n, 97 + n) for n in (5 * (1 << 20) + 3, 1 << 16, 777, 2 * (1 << 20))]
     streams.append(np.zeros(3 * (1 << 20) + 11, dtype=np.uint8))

@@ -22,12 +22,20 @@ pytestmark = pytest.mark.gpu
 
 
 def _chunker(sizes, diag):
+    """(The one-launch small-stream kernel is off: these tests drive the
+    two-kernel pipeline's resolve, whatever the stream size.)"""
     import chunkfs_amd as c
     old = os.environ.get("CHUNKFS_AMD_DIAG")
+    old_small = os.environ.get("CHUNKFS_AMD_SMALL")
     os.environ["CHUNKFS_AMD_DIAG"] = str(diag)
+    os.environ["CHUNKFS_AMD_SMALL"] = "0"
     try:
         return c.FastChunker(c.SizeParams(*sizes))
     finally:
+        if old_small is None:
+            os.environ.pop("CHUNKFS_AMD_SMALL", None)
+        else:
+            os.environ["CHUNKFS_AMD_SMALL"] = old_small
         if old is None:
             del os.environ["CHUNKFS_AMD_DIAG"]
         else:
