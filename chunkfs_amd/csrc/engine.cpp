@@ -9,6 +9,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -133,6 +134,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         e->small_pmin_ = pmin;
         if (const char *v = std::getenv("CHUNKFS_AMD_SMALL")) e->small_on_ = e->small_on_ && std::atoi(v) != 0;
         if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_ZC")) e->small_zc_ = std::atoi(v) != 0;
+        if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_FEED")) e->small_feed_ = std::atoi(v);
         char buf[256];
         std::snprintf(buf, sizeof buf,
                       "FastCDC (2020), sizes: SizeParams { min: %u, avg: %u, max: %u } "
@@ -199,6 +201,7 @@ Engine::~Engine() {
     (void)hipHostFree(h_stage_);
     if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
     (void)hipHostFree(h_ring_);
+    (void)hipHostFree(h_ready_);
     (void)hipHostFree(h_out_);
     for (auto &w : ws_win_) (void)hipFree(w);
     for (auto &e : ring_ev_)
@@ -484,24 +487,43 @@ bool Engine::small_ok(uint64_t len) const {
 }
 
 int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, size_t out_cap, uint64_t *first,
-                      hipStream_t s, bool host_input) {
+                      hipStream_t s, bool host_input, const uint8_t *feed_src, uint8_t *feed_dst,
+                      uint32_t feed_slot) {
     if (!small_mem_) {
-        HIP_TRY(hipMalloc(&small_mem_, small::scratch_bytes() + small::copy_bytes()));
+        HIP_TRY(hipMalloc(&small_mem_, small::scratch_bytes() + small::copy_bytes() + small::bstamp_bytes()));
         HIP_TRY(hipMemset(small_mem_, 0, small::scratch_bytes()));  // the ticket starts at 0
         uint32_t *b = static_cast<uint32_t *>(small_mem_);
         small_ws_.brec = reinterpret_cast<uint64_t *>(b);
         small_ws_.bcnt = b + 2 * small::kMaxBlocks * small::kBlockRecCap;
         small_ws_.ticket = small_ws_.bcnt + small::kMaxBlocks;
         small_ws_.stamp = reinterpret_cast<uint64_t *>(static_cast<char *>(small_mem_) + small::scratch_bytes() - 64);
+        small_ws_.bpub = small_ws_.stamp - small::kMaxBlocks;
         small_ws_.copy = static_cast<uint8_t *>(small_mem_) + small::scratch_bytes();
+        small_ws_.bstamp = reinterpret_cast<uint64_t *>(small_ws_.copy + small::copy_bytes());
     }
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_misc = h + 4 * h_stage_streams_;  // (the regular path's stats ++ first[] area)
     uint64_t *h_first = h_misc + p3::kStatWords;
     volatile uint64_t *done = h_misc + small::kWordDone;
     *done = 0;
-    HIP_TRY(small::launch_small(data, len, fp_, d_gear_, small_ws_, d_out, out_cap, h_misc, h_first, host_input, s));
+    small_seq_ = small_seq_ % 0xFFFFFFFEull + 1;  // 1 .. 2^32 - 2 (tags: seq << 32 | count)
+    const small::Feed feed{feed_src ? h_ready_dev_ + (size_t)feed_slot * small::kFeedPieces : nullptr, small_seq_};
+    auto feed_copy = [&]() {
+        const auto tc = std::chrono::steady_clock::now();
+        pool_->copy_feed(feed_dst, feed_src, len, size_t(1) << small::kFeedLog2,
+                         h_ready_ + (size_t)feed_slot * small::kFeedPieces, small_seq_);
+        small_copy_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
+    };
+    if (feed_src && small_feed_ == 2) feed_copy();  // (A/B: the feed copy first)
+    HIP_TRY(small::launch_small(data, len, fp_, d_gear_, small_ws_, d_out, out_cap, h_misc, h_first, host_input,
+                                feed, s));
     ++small_calls_;
+    if (feed_src && small_feed_ != 2) {
+        // The kernel is on its way (launch latency overlaps the copy): the
+        // copy pool writes the bytes piece by piece, each announced by its
+        // feed word once in memory.
+        feed_copy();
+    }
     // The last block writes the done word after a system-scope release: spin on
     // it (a call is ~20-60 us of device time), then the stream sync confirms.
     const auto t_spin = std::chrono::steady_clock::now();
@@ -528,6 +550,24 @@ int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, siz
                      (unsigned long long)(t[6] >> 42));
         for (int k = 0; k < 4; ++k)
             if (h_first[2 + k]) std::fprintf(stderr, " %.2f", (h_first[2 + k] - t[0]) / 100.0);
+        if (feed_src) std::fprintf(stderr, "; block 0 fed at %.2f; host copy %.2f us", (h_first[6] - t[0]) / 100.0,
+                                   small_copy_s_ * 1e6);
+        std::fprintf(stderr, "; round 0 added %llu entries, round 1 worked on %llu", (unsigned long long)(h_first[7] & 0xFFFF),
+                     (unsigned long long)(h_first[7] >> 16));
+        std::fprintf(stderr, "\n");
+        // per-block stamps: min / median / max of start, fed, bytes in LDS, ticket
+        const uint32_t G = (uint32_t)((len + small::kBlockBytes - 1) / small::kBlockBytes);
+        std::vector<uint64_t> bs((size_t)G * 8);
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipMemcpy(bs.data(), small_ws_.bstamp, bs.size() * 8, hipMemcpyDeviceToHost));
+        const char *nm[6] = {"fed", "loaded", "hashed(w0)", "tinfo(w0)", "drained", "ticket"};
+        std::fprintf(stderr, "  blocks (%u):", G);
+        for (int k = 0; k < 6; ++k) {
+            std::vector<double> v;
+            for (uint32_t b = 0; b < G; ++b) v.push_back(((double)bs[b * 8 + k] - (double)t[0]) / 100.0);
+            std::sort(v.begin(), v.end());
+            std::fprintf(stderr, " %s %.2f/%.2f/%.2f", nm[k], v.front(), v[v.size() / 2], v.back());
+        }
         std::fprintf(stderr, "\n");
     }
     if (h_misc[small::kWordFallback]) {

@@ -34,11 +34,18 @@ class CopyPool {
     ~CopyPool();
     static CopyPool &shared();
     void copy(void *dst, const void *src, size_t n);
+    // Streamed copy for the small kernel's feed: pieces of `piece` bytes
+    // dealt round-robin to the threads (the caller's included), each
+    // announced by ready[piece index] = seq once copied (the device reads it
+    // over PCIe while later pieces are still being copied).  Returns once
+    // every piece is announced.
+    void copy_feed(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready, uint64_t seq);
     unsigned threads() const { return (unsigned)th_.size() + 1; }
 
   private:
     void run(unsigned id);
     void part(unsigned id, unsigned parts);
+    void start(unsigned parts);  // hand the job in dst_/src_/n_ (and the feed fields) to the helpers
     std::vector<std::thread> th_;
     std::mutex m_, job_m_;
     std::condition_variable cv_;
@@ -50,6 +57,9 @@ class CopyPool {
     const uint8_t *src_ = nullptr;
     size_t n_ = 0;
     unsigned parts_ = 1;
+    size_t piece_ = 0;                      // feed jobs: piece size (0: a plain copy job)
+    volatile uint64_t *ready_ = nullptr;
+    uint64_t seq_ = 0;
 };
 
 class Engine {
@@ -126,8 +136,12 @@ class Engine {
     // (a budget was exceeded: run the regular pipeline) or a CDC_E* code.
     static constexpr int kSmallFallback = 1;
     bool small_ok(uint64_t len) const;
+    // feed_src: streamed host input -- the kernel is launched first, then the
+    // bytes are copied from feed_src into feed_dst (ring slot feed_slot, which
+    // `data` addresses) piece by piece, each piece announced by a feed word.
     int run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, size_t out_cap, uint64_t *first,
-                  hipStream_t s, bool host_input = false);
+                  hipStream_t s, bool host_input = false, const uint8_t *feed_src = nullptr,
+                  uint8_t *feed_dst = nullptr, uint32_t feed_slot = 0);
     int run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
                   cdc_chunk_t *d_out, uint64_t *first, hipStream_t s);
     // Rabin / Ultra / Leap / Seq: the segment-walk engine (walk.hip).
@@ -203,6 +217,9 @@ class Engine {
     CopyPool *pool_ = nullptr;  // CopyPool::shared()
     hipEvent_t ring_ev_[kRingSlots] = {};
     uint32_t ring_next_ = 0;
+    // Feed words of the small path's streamed input: kFeedPieces per ring
+    // slot (pinned, coherent), and their device address.
+    uint64_t *h_ready_ = nullptr, *h_ready_dev_ = nullptr;
     hipStream_t copy_stream_ = nullptr;
     hipEvent_t copy_done_ = nullptr, ws_ev_ = nullptr;
     cdc_chunk_t *h_out_ = nullptr, *d_hout_ = nullptr;
@@ -239,11 +256,16 @@ class Engine {
     // Small-stream path (small.hip): on unless CHUNKFS_AMD_SMALL=0; its input
     // straight from the pinned ring slot (no H2D copy) unless CHUNKFS_AMD_SMALL_ZC=0.
     bool small_on_ = false, small_zc_ = true;
+    // Streamed input: 1 = launch first, then the copy with feed words; 0 = the
+    // whole copy, then the launch; 2 = the feed copy, then the launch (A/B).
+    int small_feed_ = 1;
     uint32_t small_pmin_ = 0;  // min(popcount mask_s, popcount mask_l): records ~ 2^-pmin per byte
     bool small_skip_ = false;  // chunk_host's fallback call: the kernel already declined the bytes
     void *small_mem_ = nullptr;
     small::Scratch small_ws_{};
     uint64_t small_calls_ = 0, small_fallbacks_ = 0;
+    uint64_t small_seq_ = 0;      // launch sequence number (feed words, block publication tags)
+    double small_copy_s_ = 0;     // the last streamed call's host copy time
     uint64_t last_spans_ = 0;  // spans of the last FastCDC batch (debug_copy)
     uint64_t out_cap_ = 0;     // capacity of the current batch's output (resolve bound)
 

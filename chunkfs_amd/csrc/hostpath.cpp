@@ -28,6 +28,8 @@
 
 #include "engine.hpp"
 
+#include <atomic>
+
 namespace cdc {
 
 #define HIP_TRY(expr)                                                          \
@@ -77,6 +79,19 @@ CopyPool::~CopyPool() {
 }
 
 void CopyPool::part(unsigned id, unsigned parts) {
+    if (piece_) {  // feed job: pieces id, id + parts, ... each announced once in memory
+        const size_t np = (n_ + piece_ - 1) / piece_;
+        for (size_t p = id; p < np; p += parts) {
+            const size_t a = p * piece_;
+            // (plain stores: the ring slot stays in the CPU caches, where the
+            // device's PCIe reads snoop it -- non-temporal stores measured 2-3x
+            // slower for 1 MiB calls)
+            std::memcpy(dst_ + a, src_ + a, std::min(piece_, n_ - a));
+            std::atomic_thread_fence(std::memory_order_release);  // (x86: stores stay in order)
+            ready_[p] = seq_;
+        }
+        return;
+    }
     // 4 KiB-aligned part boundaries (whole pages per thread).
     const size_t step = ((n_ + parts - 1) / parts + 4095) & ~size_t(4095);
     const size_t a = std::min(n_, step * id), b = std::min(n_, a + step);
@@ -118,7 +133,31 @@ void CopyPool::copy(void *dst, const void *src, size_t n) {
     dst_ = static_cast<uint8_t *>(dst);
     src_ = static_cast<const uint8_t *>(src);
     n_ = n;
-    parts_ = (unsigned)std::min<size_t>(helpers + 1, (n + (size_t(64) << 10) - 1) >> 16);
+    piece_ = 0;
+    start((unsigned)std::min<size_t>(helpers + 1, (n + (size_t(64) << 10) - 1) >> 16));
+}
+
+void CopyPool::copy_feed(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready,
+                         uint64_t seq) {
+    const size_t np = (n + piece - 1) / piece;
+    const unsigned helpers = (unsigned)th_.size();
+    std::lock_guard<std::mutex> job(job_m_);
+    dst_ = static_cast<uint8_t *>(dst);
+    src_ = static_cast<const uint8_t *>(src);
+    n_ = n;
+    piece_ = piece;
+    ready_ = ready;
+    seq_ = seq;
+    if (helpers == 0 || np == 1) {
+        part(0, 1);
+        return;
+    }
+    start((unsigned)std::min<size_t>(helpers + 1, np));
+}
+
+void CopyPool::start(unsigned parts) {
+    const unsigned helpers = (unsigned)th_.size();
+    parts_ = parts;
     left_.store(helpers, std::memory_order_relaxed);
     {
         std::lock_guard<std::mutex> g(m_);  // (pairs with the sleepers' predicate check)
@@ -134,8 +173,14 @@ void CopyPool::copy(void *dst, const void *src, size_t n) {
 int Engine::ensure_ring() {
     if (h_ring_) return CDC_OK;
     if (!pool_) pool_ = &CopyPool::shared();
-    HIP_TRY(hipHostMalloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocDefault));
+    // Coherent (fine-grained): the small kernel reads a slot while the host is
+    // still filling it (streamed input), so the device must never cache it.
+    HIP_TRY(hipHostMalloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_ring_dev_), h_ring_, 0));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_ready_), kRingSlots * small::kFeedPieces * 8,
+                          hipHostMallocCoherent));
+    std::memset(h_ready_, 0, kRingSlots * small::kFeedPieces * 8);
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_ready_dev_), h_ready_, 0));
     for (auto &e : ring_ev_) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&copy_done_, hipEventDisableTiming));
@@ -204,10 +249,12 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
     double t1 = t0;
     bool small_tried = false;
     // FastCDC calls of the reference's size (StorageWriter's 1 MiB segments +
-    // the carried chunk): the bytes go into a pinned ring slot and the one-
-    // launch small kernel reads them there over PCIe -- no DMA, no second
-    // kernel on the call's critical path (small.hip).  A call the kernel's
-    // budgets cannot take falls through to the regular upload + pipeline.
+    // the carried chunk): the one-launch small kernel is launched first and
+    // reads the bytes over PCIe from a pinned ring slot that this thread fills
+    // meanwhile, 128 KiB at a time, each piece announced by a feed word -- the
+    // copy overlaps the launch and the reads; no DMA, no second kernel on the
+    // call's critical path (small.hip).  A call the kernel's budgets cannot
+    // take falls through to the regular upload + pipeline.
     if (algo_ == CDC_ALGO_FASTCDC && small_zc_ && !digests && small_ok(len) && len <= kRingSlot) {
         rc = ensure_host_staging(1);
         if (rc) return rc;
@@ -215,10 +262,16 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
         ring_next_ = (ring_next_ + 1) % kRingSlots;
         HIP_TRY(hipEventSynchronize(ring_ev_[k]));
         uint8_t *slot = static_cast<uint8_t *>(h_ring_) + (size_t)k * kRingSlot;
-        pool_->copy(slot, data, len);
-        t1 = now_s();
         uint64_t first[2] = {0, 0};
-        rc = run_small(h_ring_dev_ + (size_t)k * kRingSlot, len, d_hout_, need, first, own_stream_, true);
+        if (small_feed_) {
+            rc = run_small(h_ring_dev_ + (size_t)k * kRingSlot, len, d_hout_, need, first, own_stream_, true, data,
+                           slot, k);
+            t1 = t0 + small_copy_s_;
+        } else {  // (A/B: the whole copy, then the launch)
+            pool_->copy(slot, data, len);
+            t1 = now_s();
+            rc = run_small(h_ring_dev_ + (size_t)k * kRingSlot, len, d_hout_, need, first, own_stream_, true);
+        }
         HIP_TRY(hipEventRecord(ring_ev_[k], own_stream_));  // the slot is free once the kernel retires
         if (rc < 0) return rc;
         if (rc == CDC_OK) count = (int64_t)first[1];

@@ -1,0 +1,3 @@
+export TMPDIR=/tmp
+timeout -k 10 120 python -u tools/small_stamps.py 1048576 2>&1 | grep -v amdgpu.ids || exit 1
+CHUNKFS_AMD_SMALL_FEED=0 timeout -k 10 120 python -u tools/small_stamps.py 1048576 2>&1 | grep -v amdgpu.ids || exit 1
