@@ -949,6 +949,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     bool rsum = walk::bits_write_summary(wp_);  // quiet runs (CHUNKFS_AMD_QUIET=0: off, A/B)
     if (const char *q = std::getenv("CHUNKFS_AMD_QUIET")) rsum = rsum && std::atoi(q) != 0;
     const size_t oRS = take(rsum ? S * (size_t)wp_.seg_words / 8 * (algo_ == CDC_ALGO_RABIN ? 2 : 1) : 0);  // quiet-run summary
+    const size_t oQS = take(rsum ? S : 0);  // and per segment
     const size_t cc = wp_.links ? wp_.ccap : 0;                          // link mode
     const size_t oCN = take(S * 4), oCP = take(S * cc * 4), oLN = take(S * cc * 8), oLI = take(S * cc * 4);
     const size_t vc = wp_.links ? S * 8 : 0;
@@ -978,6 +979,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wp_.jt = jt ? reinterpret_cast<uint8_t *>(b + oJT) : nullptr;
     wp_.jt8 = jt ? reinterpret_cast<uint16_t *>(b + oJ8) : nullptr;
     wp_.rsum = rsum ? reinterpret_cast<uint64_t *>(b + oRS) : nullptr;
+    wp_.qseg = rsum ? reinterpret_cast<uint8_t *>(b + oQS) : nullptr;
     wp_.ccnt = reinterpret_cast<uint32_t *>(b + oCN);
     wp_.cpos = reinterpret_cast<uint32_t *>(b + oCP);
     wp_.lnext = reinterpret_cast<uint64_t *>(b + oLN);

@@ -1485,8 +1485,29 @@ __device__ bool wrewalk(uint64_t x, uint64_t g, uint64_t seg_end, uint64_t len, 
     return c != x_old;
 }
 
+template <int kAlgo>
+__device__ uint64_t serial_run(const StreamTable &st, const WalkParams &wp, const WalkState &ws, const WBm &B,
+                               const uint64_t *rs, uint64_t g0, uint64_t g1, uint64_t g, uint64_t x, uint64_t len,
+                               uint32_t lane, uint64_t &xe, const uint64_t *sE = nullptr,
+                               const uint64_t *sX = nullptr, bool *capped = nullptr, uint64_t *xold = nullptr);
+
+// A fix-up round's segment g (scheduled: its snapshot entry is not its
+// predecessor's snapshot exit) leaves its re-walk to its predecessor's chain
+// when both are wholly quiet in a common kind (qseg) and the predecessor is
+// scheduled too: that chain takes the whole quiet stretch at once
+// (serial_run), instead of every segment of the stretch re-walking its own
+// stale phase (UltraCDC's chunk length does not divide the segment size, so
+// inside a zero-filled region every segment starts out of phase).  off: g's
+// offset in its stream.
+__device__ __forceinline__ bool defers(const StreamTable &st, const WalkParams &wp, const WalkState &ws, uint64_t g,
+                                       uint64_t off) {
+    if (!wp.qseg || off < (2ull << st.span_log2)) return false;  // (g - 1 is the stream's first: never scheduled)
+    return (wp.qseg[g] & wp.qseg[g - 1]) != 0 && ws.Es[g - 1] != ws.Xs[g - 2];
+}
+
 // fix_kernel with a wave per segment: same schedule (snapshots Es / Xs, run
-// ahead into unscheduled successors), wave-cooperative re-walks.
+// ahead into unscheduled successors), wave-cooperative re-walks; a chain that
+// enters a quiet run crosses every segment the run covers at once.
 template <int kAlgo>
 __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
     if (round_stops(ws.gate)) return;  // the previous round settled everything (or went quiet)
@@ -1500,6 +1521,13 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     if (off == 0) return;  // a stream's first segment starts exactly at 0
     uint64_t x = ws.Xs[g - 1];
     if (ws.Es[g] == x) return;
+    if (defers(st, wp, ws, g, off)) {  // the chain of an earlier segment crosses this one this round
+        if (lane == 0) {
+            atomicAdd(&ws.flags[0], 1ull);  // (one more round checks it)
+            atomicMin(&ws.flags[2], (unsigned long long)(g - 1));
+        }
+        return;
+    }
     const uint64_t len = st.lens[si];
     const uint64_t span = 1ull << st.span_log2;
     __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
@@ -1509,12 +1537,25 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     const uint64_t *rs = wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t gg = g;
+    const uint64_t g0 = st.span_base[si], g1 = st.span_base[si + 1];
     for (uint32_t k = 0;; ++k) {
-        const uint64_t seg_end = min(off + span, len);
         if (lane == 0) atomicAdd(&ws.flags[3], 1ull);  // segments re-walked (statistics)
         uint64_t xo;
-        bool qr;
-        const bool changed = wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, lane, xo, qr);
+        bool qr = false, changed;
+        uint64_t ge = gg;
+        if (rs) {  // a quiet run from x through whole segments: all of them at once
+            bool capped = false;
+            uint64_t xold = 0;
+            ge = serial_run<kAlgo>(st, wp, ws, B, rs, g0, g1, gg, x, len, lane, xo, ws.Es, ws.Xs, &capped, &xold);
+            if (ge > gg) {
+                gg = ge - 1;
+                off = (gg - g0) << st.span_log2;
+                changed = xo != xold;
+                qr = capped;  // stopped inside the quiet run: phase-locked, for the hand-off count
+            }
+        }
+        const uint64_t seg_end = min(off + span, len);
+        if (ge == gg) changed = wrewalk<kAlgo>(x, gg, seg_end, len, B, rs, wp, ws, lane, xo, qr);
         if (!changed) break;
         if (seg_end >= len) break;  // the stream's last segment: no successor
         if (k + 1 >= wp.ahead || ws.Es[gg + 1] != ws.Xs[gg]) {
@@ -1537,23 +1578,41 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     }
 }
 
-// The in-order pass inside a quiet run: the chain from x (segment g's entry)
-// takes k chunks of length L; every segment that ends at or before the run's
-// covered part gets its list, entry, count and exit written directly (lanes
-// over chunks, then over segments).  Returns the first segment the run does
-// not cover whole (g: none), xe = its entry.
+// A quiet run through whole segments (the in-order pass, and the fix-up
+// rounds' phase propagation): the chain from x (segment g's entry) takes k
+// chunks of length L; every segment that ends at or before the run's covered
+// part gets its list, entry, count and exit written directly (lanes over
+// chunks, then over segments) -- a region settles as soon as its entry phase
+// is known, instead of one segment per fix-up round.  In a fix-up round (sE /
+// sX: the round's snapshots) the run stops before any later segment that the
+// round re-walks on its own (so no two waves write one segment).  Returns the
+// first segment the run does not cover whole (g: none), xe = its entry.
 template <int kAlgo>
 __device__ uint64_t serial_run(const StreamTable &st, const WalkParams &wp, const WalkState &ws, const WBm &B,
                                const uint64_t *rs, uint64_t g0, uint64_t g1, uint64_t g, uint64_t x, uint64_t len,
-                               uint32_t lane, uint64_t &xe) {
+                               uint32_t lane, uint64_t &xe, const uint64_t *sE, const uint64_t *sX, bool *capped,
+                               uint64_t *xold) {
     uint64_t L;
     uint64_t k = quiet_run_k<kAlgo>(0, B, rs, x, len, len, wp, lane, L);
     if constexpr (kQuietKinds<kAlgo> > 1)
         if (k < 2) k = quiet_run_k<kAlgo>(1, B, rs, x, len, len, wp, lane, L);
     const uint64_t ce = x + k * L;
     const uint32_t sl = st.span_log2;
-    const uint64_t ie = min(ce >> sl, g1 - g0), i0 = g - g0;
+    uint64_t ie = min(ce >> sl, g1 - g0);
+    const uint64_t i0 = g - g0;
     if (k < 2 || ie <= i0) return g;
+    if (sE)  // the first later segment this round re-walks by itself (scheduled, not deferring)
+        for (uint64_t b = i0 + 1; b < ie; b += 64) {
+            const uint64_t i = b + lane;
+            const uint64_t m = __ballot(i < ie && sE[g0 + i] != sX[g0 + i - 1] &&
+                                        !defers(st, wp, ws, g0 + i, i << sl));
+            if (m) {
+                ie = b + (uint64_t)__builtin_ctzll(m);
+                if (capped) *capped = true;
+                break;
+            }
+        }
+    if (xold) *xold = ws.X[g0 + ie - 1];  // (before the writes below)
     const uint64_t send = min(ie << sl, len);  // the covered segments end here
     const uint64_t jtot = send > x ? (send - x + L - 1) / L : 0;  // run starts inside them
     for (uint64_t j = lane; j < jtot; j += 64) {
@@ -2396,6 +2455,28 @@ bool bits_write_summary(const WalkParams &wp) {
     }
 }
 
+// Per segment: which quiet kinds hold at every position (qseg, see WalkParams).
+template <int kAlgo>
+__global__ __launch_bounds__(256) void qseg_kernel(const StreamTable st, const WalkParams wp) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= st.total_spans) return;
+    uint32_t si;
+    uint64_t off;
+    locate(st, g, si, off);
+    uint32_t m = 0;
+    if (g + 1 < st.span_base[si + 1]) {  // (a stream's last segment: 0)
+        const uint64_t sw = wp.seg_words >> 6;  // summary words per segment and kind
+#pragma unroll
+        for (int kind = 0; kind < kQuietKinds<kAlgo>; ++kind) {
+            bool all = true;
+            for (uint64_t i = lane; i < sw; i += 64) all = all && wp.rsum[(g * sw + i) * kQuietKinds<kAlgo> + kind] == ~0ull;
+            if (__ballot(!all) == 0) m |= 1u << kind;
+        }
+    }
+    if (lane == 0) wp.qseg[g] = (uint8_t)m;
+}
+
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s) {
     if (!st.total_spans || !wp.nbm) return hipSuccess;
     const uint64_t pieces = st.total_spans << (st.span_log2 - wp.piece_log2);
@@ -2413,6 +2494,13 @@ hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t 
     else return hipErrorInvalidValue;
     if (wp.algo == 5 && wp.wave && wp.jt && wp.piece_log2 >= 12)  // LeapCDC word tables
         jtab_kernel<<<(unsigned)((pieces + 3) / 4), 256, 0, s>>>(st, wp);
+    if (wp.rsum && wp.qseg) {
+        const unsigned qb = (unsigned)((st.total_spans + 3) / 4);
+        if (wp.algo == 2) qseg_kernel<2><<<qb, 256, 0, s>>>(st, wp);
+        else if (wp.algo == 4) qseg_kernel<4><<<qb, 256, 0, s>>>(st, wp);
+        else if (wp.algo == 5) qseg_kernel<5><<<qb, 256, 0, s>>>(st, wp);
+        else qseg_kernel<6><<<qb, 256, 0, s>>>(st, wp);
+    }
     return hipGetLastError();
 }
 

@@ -79,6 +79,11 @@ struct WalkParams {
     // nullptr when the bitmap pass in use does not write it
     // (bits_write_summary).
     uint64_t *rsum;
+    // ... and per segment, bit k: every summary word of quiet kind k is all
+    // quiet (a stream's last segment: 0), from qseg_kernel after the bitmap
+    // pass.  A fix-up round lets one chain cross a stretch of such segments
+    // whole (walk.hip serial_run); nullptr with rsum.
+    uint8_t *qseg;
 };
 
 constexpr uint32_t kNoCand = 0xFFFFFFFFu;
