@@ -1695,18 +1695,32 @@ __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, cons
 // the stream start are never tested by the walks (they need min >= 48 / 8 /
 // 32), nor are bits at or past the stream end.
 
+// Global (address space 1) loads: through a generic pointer these compile to
+// flat_load_*, which count on lgkmcnt as well as vmcnt, so every wait for an
+// LDS table lookup would also wait for the next step's prefetched bytes.
+typedef unsigned int wu32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) wu32x4 gw_u32x4;
+typedef const __attribute__((address_space(1))) uint8_t gw_u8;
+
 __device__ __forceinline__ uint4 load16_guarded(const uint8_t *base, uint64_t a, uint64_t len) {
-    if (a + 16 <= len) return *reinterpret_cast<const uint4 *>(base + a);
+    if (a + 16 <= len) {
+        const wu32x4 v = *(gw_u32x4 *)(base + a);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
     uint32_t t[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j)
-        if (a + j < len) t[j >> 2] |= (uint32_t)base[a + j] << (8 * (j & 3));
+        if (a + j < len) t[j >> 2] |= (uint32_t)((gw_u8 *)base)[a + j] << (8 * (j & 3));
     return make_uint4(t[0], t[1], t[2], t[3]);
 }
 
 __device__ __forceinline__ uint32_t byte_of(const uint4 &v, int j) {
     const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
     return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t word_of(const uint4 &v, int w) {
+    return w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
 }
 
 __device__ __forceinline__ uint64_t lo64(const uint4 &v) { return ((uint64_t)v.y << 32) | v.x; }
@@ -2018,17 +2032,27 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
 constexpr int kRabinReps = CDC_RABIN_REPS;
 constexpr int kRabinWaves = CDC_RABIN_WAVES;  // pieces per block (64 KiB of tables shared by 8 waves)
 
+typedef const __attribute__((address_space(3))) uint64_t lds_w64;
+typedef const __attribute__((address_space(3))) char lds_wchar;
+
 __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTable st, const WalkParams wp) {
-    __shared__ uint64_t rt[2 * 256 * kRabinReps];  // [table][entry][replica]: mod, out
-    for (int i = threadIdx.x; i < 2 * 256 * kRabinReps; i += 64 * kRabinWaves) {
-        const int t = i / (256 * kRabinReps), e = (i / kRabinReps) & 255;
-        rt[i] = wp.tabs[t * 256 + e];
+    // entry e at e * 256 bytes: 16 replicas of mod[e], then 16 of out[e]; a
+    // lane's replica offset is one byte, so each lookup address is one v_perm
+    // (out: the leaving byte) or one v_lshl_or (mod: the digest's top byte).
+    // (Two interleaved chains per lane -- more independent lookups in flight
+    // -- need ~2x the registers and spilled at the 128 VGPRs of 16 waves / CU.)
+    __shared__ uint64_t rt[256 * 32];
+    static_assert(kRabinReps == 16, "rbits_kernel: 16 replicas per table");
+    for (int i = threadIdx.x; i < 256 * 32; i += 64 * kRabinWaves) {
+        const int e = i >> 5, k = i & 31;
+        rt[i] = wp.tabs[(k < 16 ? 0 : 256) + e];
     }
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
     if (!piece_of(st, wp, (uint64_t)blockIdx.x * kRabinWaves + (threadIdx.x >> 6), pc)) return;
-    const uint64_t *tmod = rt + (lane & (kRabinReps - 1)), *tout = tmod + 256 * kRabinReps;
+    const uint32_t om = (lane & 15) * 8, oo = 128 + om;  // this lane's mod / out replica
+    lds_wchar *tb = (lds_wchar *)rt;
     const uint64_t len = st.lens[pc.si];
     const uint8_t *base = st.ptrs[pc.si];
     const uint64_t w = (1ull << wp.piece_log2) >> 6;  // bytes per lane (a multiple of 64)
@@ -2042,12 +2066,15 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
         auto step16 = [&](const uint4 &cur, const uint4 &old, uint32_t &bits, int sh, bool test) {
     #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const uint64_t o = tout[byte_of(old, j) * kRabinReps];
+                const uint32_t ow = word_of(old, j >> 2), cw = word_of(cur, j >> 2);
+                const uint32_t ao = __builtin_amdgcn_perm(oo, ow, 0x0c0c0004u | ((uint32_t)(j & 3) << 8));
+                const uint64_t o = *reinterpret_cast<lds_w64 *>(tb + ao);
                 lo ^= (uint32_t)o;
                 hi ^= (uint32_t)(o >> 32);
-                const uint64_t m = tmod[(hi >> tsh) * kRabinReps];
+                const uint64_t m = *reinterpret_cast<lds_w64 *>(tb + (((hi >> tsh) << 8) | om));
                 hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
-                lo = ((lo << 8) | byte_of(cur, j)) ^ (uint32_t)m;
+                // (lo << 8) | the entering byte, one v_perm
+                lo = __builtin_amdgcn_perm(lo, cw, 0x06050400u | (uint32_t)(j & 3)) ^ (uint32_t)m;
                 if (test) bits |= min(lo & rmask, 1u) << (sh + j);
             }
         };
