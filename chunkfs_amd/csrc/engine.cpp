@@ -135,6 +135,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         if (const char *v = std::getenv("CHUNKFS_AMD_SMALL")) e->small_on_ = e->small_on_ && std::atoi(v) != 0;
         if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_ZC")) e->small_zc_ = std::atoi(v) != 0;
         if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_FEED")) e->small_feed_ = std::atoi(v);
+        if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_FEED_POOL")) e->small_feed_pool_ = std::atoi(v) != 0;
         char buf[256];
         std::snprintf(buf, sizeof buf,
                       "FastCDC (2020), sizes: SizeParams { min: %u, avg: %u, max: %u } "
@@ -510,8 +511,20 @@ int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, siz
     const small::Feed feed{feed_src ? h_ready_dev_ + (size_t)feed_slot * small::kFeedPieces : nullptr, small_seq_};
     auto feed_copy = [&]() {
         const auto tc = std::chrono::steady_clock::now();
-        pool_->copy_feed(feed_dst, feed_src, len, size_t(1) << small::kFeedLog2,
-                         h_ready_ + (size_t)feed_slot * small::kFeedPieces, small_seq_);
+        volatile uint64_t *ready = h_ready_ + (size_t)feed_slot * small::kFeedPieces;
+        if (small_feed_pool_) {
+            // the calling thread and whichever copy-pool helpers are awake
+            // claim the pieces (work stealing: never a wait for a sleeper)
+            pool_->copy_feed(feed_dst, feed_src, len, size_t(1) << small::kFeedLog2, ready, small_seq_);
+        } else {
+            // (A/B: the calling thread alone)
+            const uint64_t piece = 1ull << small::kFeedLog2;
+            for (uint64_t off = 0; off < len; off += piece) {
+                std::memcpy(feed_dst + off, feed_src + off, std::min(piece, len - off));
+                std::atomic_thread_fence(std::memory_order_release);  // (x86: stores stay in order)
+                ready[off >> small::kFeedLog2] = small_seq_;
+            }
+        }
         small_copy_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
     };
     if (feed_src && small_feed_ == 2) feed_copy();  // (A/B: the feed copy first)

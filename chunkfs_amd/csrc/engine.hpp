@@ -34,31 +34,30 @@ class CopyPool {
     ~CopyPool();
     static CopyPool &shared();
     void copy(void *dst, const void *src, size_t n);
-    // Streamed copy for the small kernel's feed: pieces of `piece` bytes
-    // dealt round-robin to the threads (the caller's included), each
-    // announced by ready[piece index] = seq once copied (the device reads it
-    // over PCIe while later pieces are still being copied).  Returns once
-    // every piece is announced.
+    // Streamed copy for the small kernel's feed: pieces of `piece` bytes,
+    // claimed by the caller and the awake helpers, each announced by
+    // ready[piece index] = seq once copied (the device reads it over PCIe
+    // while later pieces are still being copied).  Returns once every piece
+    // is announced.
     void copy_feed(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready, uint64_t seq);
     unsigned threads() const { return (unsigned)th_.size() + 1; }
 
   private:
     void run(unsigned id);
-    void part(unsigned id, unsigned parts);
-    void start(unsigned parts);  // hand the job in dst_/src_/n_ (and the feed fields) to the helpers
+    void work();  // claim and copy pieces until none is left
+    void job(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready, uint64_t seq);
     std::vector<std::thread> th_;
     std::mutex m_, job_m_;
     std::condition_variable cv_;
     unsigned spin_us_ = 200;
     std::atomic<uint64_t> gen_{0};
-    std::atomic<unsigned> left_{0};
-    std::atomic<bool> stop_{false};
+    std::atomic<bool> stop_{false}, open_{false};
+    std::atomic<unsigned> active_{0};  // helpers inside the current job
+    std::atomic<size_t> next_{0}, done_{0};  // next piece to claim, pieces copied
     uint8_t *dst_ = nullptr;
     const uint8_t *src_ = nullptr;
-    size_t n_ = 0;
-    unsigned parts_ = 1;
-    size_t piece_ = 0;                      // feed jobs: piece size (0: a plain copy job)
-    volatile uint64_t *ready_ = nullptr;
+    size_t n_ = 0, piece_ = 0, np_ = 0;
+    volatile uint64_t *ready_ = nullptr;  // feed words (nullptr: a plain copy)
     uint64_t seq_ = 0;
 };
 
@@ -259,6 +258,7 @@ class Engine {
     // Streamed input: 1 = launch first, then the copy with feed words; 0 = the
     // whole copy, then the launch; 2 = the feed copy, then the launch (A/B).
     int small_feed_ = 1;
+    bool small_feed_pool_ = true;  // the feed copy on the copy pool (CHUNKFS_AMD_SMALL_FEED_POOL=0: caller only, A/B)
     uint32_t small_pmin_ = 0;  // min(popcount mask_s, popcount mask_l): records ~ 2^-pmin per byte
     bool small_skip_ = false;  // chunk_host's fallback call: the kernel already declined the bytes
     void *small_mem_ = nullptr;

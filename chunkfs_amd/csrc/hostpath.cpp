@@ -78,27 +78,29 @@ CopyPool::~CopyPool() {
     for (auto &t : th_) t.join();
 }
 
-void CopyPool::part(unsigned id, unsigned parts) {
-    if (piece_) {  // feed job: pieces id, id + parts, ... each announced once in memory
-        const size_t np = (n_ + piece_ - 1) / piece_;
-        for (size_t p = id; p < np; p += parts) {
-            const size_t a = p * piece_;
-            // (plain stores: the ring slot stays in the CPU caches, where the
-            // device's PCIe reads snoop it -- non-temporal stores measured 2-3x
-            // slower for 1 MiB calls)
-            std::memcpy(dst_ + a, src_ + a, std::min(piece_, n_ - a));
+// Work stealing: a job is n bytes in pieces; the caller and every helper
+// that is awake claim pieces from one counter, so a call never waits for a
+// sleeping helper (in StorageWriter's loop the helpers sleep between calls:
+// hashing and index inserts take longer than their spin).  A helper joins
+// only while the job is open; the caller closes it once every piece is done
+// and returns when no helper is still inside.
+void CopyPool::work() {
+    const size_t np = np_;
+    for (size_t p; (p = next_.fetch_add(1, std::memory_order_relaxed)) < np;) {
+        const size_t a = p * piece_;
+        // (plain stores: the ring slot stays in the CPU caches, where the
+        // device's PCIe reads snoop it -- non-temporal stores measured 2-3x
+        // slower for 1 MiB calls)
+        std::memcpy(dst_ + a, src_ + a, std::min(piece_, n_ - a));
+        if (ready_) {
             std::atomic_thread_fence(std::memory_order_release);  // (x86: stores stay in order)
             ready_[p] = seq_;
         }
-        return;
+        done_.fetch_add(1, std::memory_order_release);
     }
-    // 4 KiB-aligned part boundaries (whole pages per thread).
-    const size_t step = ((n_ + parts - 1) / parts + 4095) & ~size_t(4095);
-    const size_t a = std::min(n_, step * id), b = std::min(n_, a + step);
-    if (b > a) std::memcpy(dst_ + a, src_ + a, b - a);
 }
 
-void CopyPool::run(unsigned id) {
+void CopyPool::run(unsigned) {
     uint64_t seen = 0;
     for (;;) {
         // spin briefly for the next job (a streaming write hands over a
@@ -118,54 +120,48 @@ void CopyPool::run(unsigned id) {
         }
         if (stop_.load()) return;
         seen = g;
-        if (id < parts_) part(id, parts_);
-        left_.fetch_sub(1, std::memory_order_acq_rel);
+        active_.fetch_add(1, std::memory_order_seq_cst);
+        if (open_.load(std::memory_order_seq_cst)) work();  // (a closed job: nothing to touch)
+        active_.fetch_sub(1, std::memory_order_seq_cst);
     }
 }
 
-void CopyPool::copy(void *dst, const void *src, size_t n) {
-    const unsigned helpers = (unsigned)th_.size();
-    if (n < (size_t(256) << 10) || helpers == 0) {  // not worth a hand-off
-        std::memcpy(dst, src, n);
-        return;
-    }
-    std::lock_guard<std::mutex> job(job_m_);  // one job at a time (handles on several threads share the pool)
-    dst_ = static_cast<uint8_t *>(dst);
-    src_ = static_cast<const uint8_t *>(src);
-    n_ = n;
-    piece_ = 0;
-    start((unsigned)std::min<size_t>(helpers + 1, (n + (size_t(64) << 10) - 1) >> 16));
-}
-
-void CopyPool::copy_feed(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready,
-                         uint64_t seq) {
-    const size_t np = (n + piece - 1) / piece;
-    const unsigned helpers = (unsigned)th_.size();
-    std::lock_guard<std::mutex> job(job_m_);
+void CopyPool::job(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready, uint64_t seq) {
+    std::lock_guard<std::mutex> jl(job_m_);  // one job at a time (handles on several threads share the pool)
     dst_ = static_cast<uint8_t *>(dst);
     src_ = static_cast<const uint8_t *>(src);
     n_ = n;
     piece_ = piece;
+    np_ = (n + piece - 1) / piece;
     ready_ = ready;
     seq_ = seq;
-    if (helpers == 0 || np == 1) {
-        part(0, 1);
-        return;
+    next_.store(0, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
+    if (!th_.empty() && np_ > 1) {
+        {
+            std::lock_guard<std::mutex> g(m_);  // (pairs with the sleepers' predicate check)
+            open_.store(true, std::memory_order_seq_cst);
+            gen_.fetch_add(1, std::memory_order_acq_rel);
+        }
+        cv_.notify_all();
     }
-    start((unsigned)std::min<size_t>(helpers + 1, np));
+    work();
+    while (done_.load(std::memory_order_acquire) < np_) __builtin_ia32_pause();  // pieces a helper holds
+    open_.store(false, std::memory_order_seq_cst);
+    while (active_.load(std::memory_order_seq_cst) != 0) __builtin_ia32_pause();
 }
 
-void CopyPool::start(unsigned parts) {
-    const unsigned helpers = (unsigned)th_.size();
-    parts_ = parts;
-    left_.store(helpers, std::memory_order_relaxed);
-    {
-        std::lock_guard<std::mutex> g(m_);  // (pairs with the sleepers' predicate check)
-        gen_.fetch_add(1, std::memory_order_acq_rel);
+void CopyPool::copy(void *dst, const void *src, size_t n) {
+    if (n < (size_t(256) << 10) || th_.empty()) {  // not worth a hand-off
+        std::memcpy(dst, src, n);
+        return;
     }
-    cv_.notify_all();
-    part(0, parts_);
-    while (left_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    job(dst, src, n, size_t(256) << 10, nullptr, 0);
+}
+
+void CopyPool::copy_feed(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready,
+                         uint64_t seq) {
+    job(dst, src, n, piece, ready, seq);
 }
 
 // ---- host boundary --------------------------------------------------------------

@@ -11,7 +11,21 @@ import numpy as np  # noqa: E402
 import chunkfs_amd as c  # noqa: E402
 from chunkfs_amd.synthetic import splitmix64_bytes  # noqa: E402
 
-sizes = [int(x) for x in sys.argv[1:]] or [1 << 20, (1 << 20) + 12000, 4 << 20, 16 << 20]
+gap_us = 0.0  # --gap-us N: busy work between calls (StorageWriter hashes and indexes between its calls)
+argv = sys.argv[1:]
+if "--gap-us" in argv:
+    i = argv.index("--gap-us")
+    gap_us = float(argv[i + 1])
+    del argv[i:i + 2]
+sizes = [int(x) for x in argv] or [1 << 20, (1 << 20) + 12000, 4 << 20, 16 << 20]
+
+
+def gap():
+    if gap_us > 0:
+        t = time.perf_counter() + gap_us * 1e-6
+        while time.perf_counter() < t:
+            pass
+
 ch = c.FastChunker(c.SizeParams(4096, 8192, 16384))
 data = splitmix64_bytes(max(sizes), 9)
 for n in sizes:
@@ -22,8 +36,9 @@ for n in sizes:
     t0 = time.perf_counter()
     reps = 50
     for _ in range(reps):
+        gap()
         ch.chunk_array(buf)
-    el = (time.perf_counter() - t0) / reps
+    el = (time.perf_counter() - t0) / reps - gap_us * 1e-6
     st1 = c.host_stats(ch)
     t = ch.last_timing()
     print(f"n={n:9d}  {el * 1e6:8.1f} us/call  {n / el / 2**30:6.2f} GiB/s  small "
