@@ -727,6 +727,26 @@ __global__ __launch_bounds__(kThreads, 1) void small_kernel(const uint8_t *__res
                             rk = nx2 == nx + Rn.rem && Rn.rem == fp.max ? run_len(Q.rec, nrec, hint, fp, n, nx2) : 1;
                         }
                     }
+                    // A single start after the head (a max cut after a max
+                    // cut, or a truncated hit): its link too, now -- one more
+                    // round trip in this lane instead of a whole round.
+                    uint32_t rl = kNone, rt = kTruncUnknown;
+                    if (rk == 1) {
+                        if (n - rp <= fp.min) {
+                            rl = kEnd;
+                        } else {
+                            const Regime Rp = regime(fp, rp, n);
+                            rt = kTruncNone;
+                            if (Rp.tl > Rp.a0) {
+                                uint32_t wp2[13];
+                                trunc_load(tdata, tcap, rp + Rp.a0, wp2);
+                                rt = trunc_eval(wp2, rp + Rp.a0, Rp, fp, L.tab, rep);
+                            }
+                            uint32_t r3;
+                            const uint64_t nx3 = link_from(Q.rec, nrec, hint, rp, Rp, rt, &r3);
+                            rl = nx3 >= n ? kEnd : r3 != kNone ? r3 : kNone;
+                        }
+                    }
                     const uint32_t tot = 1u + rk;
                     const uint32_t b = atomicAdd(&L.nent, tot);
                     if (b + tot > kEntCap) {
@@ -740,8 +760,8 @@ __global__ __launch_bounds__(kThreads, 1) void small_kernel(const uint8_t *__res
                         Q.ehint[b] = (uint16_t)hint;
                         for (uint32_t j = 0; j < rk; ++j) {
                             Q.epos[b + 1 + j] = (uint32_t)(rp + (uint64_t)j * fp.max);
-                            Q.etr[b + 1 + j] = kTruncUnknown;
-                            Q.enx[b + 1 + j] = j + 1 < rk ? b + 2 + j : kNone;
+                            Q.etr[b + 1 + j] = rk == 1 && rl != kNone ? (uint8_t)rt : (uint8_t)kTruncUnknown;
+                            Q.enx[b + 1 + j] = j + 1 < rk ? b + 2 + j : rk == 1 ? rl : kNone;
                             Q.tent[b + 1 + j] = j + 1 < rk ? 1 : 0;
                             Q.ehint[b + 1 + j] = (uint16_t)hint;
                         }
