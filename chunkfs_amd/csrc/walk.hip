@@ -769,10 +769,49 @@ struct WBm {
     }
 };
 
+// The wave's index in its block, as a wave-uniform (SGPR) value: segment
+// indices, offsets and chain positions derived from it stay scalar, instead of
+// the compiler's divergent (VGPR, exec-masked) form of threadIdx.x >> 6.
+__device__ __forceinline__ uint32_t wave_id() { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 __device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
     return ((uint64_t)hi << 32) | lo;
+}
+
+// DPP lane moves (no LDS round trip, unlike __shfl_up's ds_bpermute): lanes
+// the control leaves without a source (or rows the row mask disables) get old.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kCtrl, kRowMask, 0xF, false);
+}
+
+// wave_shr:1 -- lane i receives lane i-1, lane 0 gets fill.
+__device__ __forceinline__ uint32_t wave_shr1_32(uint32_t v, uint32_t fill) { return dpp32<0x138, 0xF>(v, fill); }
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v, uint64_t fill) {
+    return ((uint64_t)wave_shr1_32((uint32_t)(v >> 32), (uint32_t)(fill >> 32)) << 32) |
+           wave_shr1_32((uint32_t)v, (uint32_t)fill);
+}
+
+// Inclusive prefix sum over the wave: row_shr 1/2/4/8 within rows of 16 lanes,
+// then row_bcast 15 (rows 1, 3) and 31 (rows 2, 3) carry the earlier rows.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp32<0x111, 0xF>(v, 0);
+    v += dpp32<0x112, 0xF>(v, 0);
+    v += dpp32<0x114, 0xF>(v, 0);
+    v += dpp32<0x118, 0xF>(v, 0);
+    v += dpp32<0x142, 0xA>(v, 0);
+    v += dpp32<0x143, 0xC>(v, 0);
+    return v;
+}
+
+// One step of UltraCDC's repeat-map scan: (fa, fv) after the source lane's map.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void ultra_map_step(uint32_t &fa, uint32_t &fv) {
+    const uint32_t pa = dpp32<kCtrl, kRowMask>(fa, 1u), pv = dpp32<kCtrl, kRowMask>(fv, 0u);
+    fv = fa ? pv + fv : fv;
+    fa &= pa;
 }
 
 // Bits 0, 8, ..., 56 of x (others zero) gathered into bits 0..7.
@@ -838,18 +877,17 @@ __device__ uint64_t wcut_ultra(const WBm &B, uint64_t s, uint64_t n, const WalkP
         const uint32_t lead = (uint32_t)__builtin_ctz(~r);                     // leading repeats (<= 8)
         const uint32_t z = ~r & 0xFFu;
         uint32_t fa = r == 0xFFu, fv = fa ? 8u : (uint32_t)__builtin_clz(z) - 24u;  // trailing repeats
-        // inclusive scan of the maps (composition: later lane after earlier)
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t pa = (uint32_t)__shfl_up((int)fa, o), pv = (uint32_t)__shfl_up((int)fv, o);
-            if (lane >= (uint32_t)o) {
-                fv = fa ? pv + fv : fv;
-                fa = fa & pa;
-            }
-        }
+        // inclusive scan of the maps (composition: later lane after earlier),
+        // DPP steps as wave_incl_sum; lanes without a source get the identity
+        // map (all repeats, length 0)
+        ultra_map_step<0x111, 0xF>(fa, fv);
+        ultra_map_step<0x112, 0xF>(fa, fv);
+        ultra_map_step<0x114, 0xF>(fa, fv);
+        ultra_map_step<0x118, 0xF>(fa, fv);
+        ultra_map_step<0x142, 0xA>(fa, fv);
+        ultra_map_step<0x143, 0xC>(fa, fv);
         const uint32_t cout = fa ? lec + fv : fv;
-        const uint32_t up = (uint32_t)__shfl_up((int)cout, 1);
-        const uint32_t cin = lane ? up : lec;
+        const uint32_t cin = wave_shr1_32(cout, lec);
         const uint32_t tb0 = cin >= CDC_ULTRA_LEST - 1 ? 0u : CDC_ULTRA_LEST - 1 - cin;
         const uint32_t tB = tb0 < lead ? tb0 : 8u;
         const uint32_t tA = (uint32_t)__builtin_ctz(a_hit | 0x100u);
@@ -1031,6 +1069,10 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// The wave walks are issue-bound, not latency-bound: one scalar unit per CU
+// serves all 16 resident waves, so every restart's instruction count is paid
+// 16 times over (a scalar 64-bit select bisection was ~65 SALU instructions of
+// a restart's ~90; the lane-parallel select is 5 VALU + 2 SALU).
 // SeqCDC over bitmap 0 (pair p in the mode's direction), a window of 4096
 // positions per load (lane l on positions 64l .. 64l+63 of it).  From a
 // restart point t0 (the chunk's min, or a jump's landing) the rule is two
@@ -1044,40 +1086,54 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
 __device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
+#ifdef CDC_EXP_SEQ_NOJUMP  // (timing experiment: no jumps)
+    const uint32_t L = wp.seq_len, TT = 1u << 20, J = wp.seq_jump;
+#else
     const uint32_t L = wp.seq_len, TT = wp.seq_trig, J = wp.seq_jump;
+#endif
     uint64_t i = wp.min;        // window start (relative to s)
     uint32_t cnt = 0, opp = 0;  // run / opposing pairs carried into the window
+    const uint64_t pmask = lane == 63 ? ~0ull : (2ull << lane) - 1;
     while (i < end) {
         const uint64_t lim = end - i;  // valid positions of the window: t < lim
         const uint64_t tl = 64ull * lane;
         const uint64_t vm = tl >= lim ? 0ull : (lim - tl >= 64 ? ~0ull : (1ull << (lim - tl)) - 1);
+#ifdef CDC_EXP_SEQ_NOLOAD  // (timing experiment: synthetic bits instead of the bitmap)
+        uint64_t hx = (s + i + tl) * 0x9E3779B97F4A7C15ull;
+        hx ^= hx >> 29;
+        hx *= 0xBF58476D1CE4E5B9ull;
+        const uint64_t y = (hx ^ (hx >> 32)) & vm;
+#else
         const uint64_t y = B.bits64(1, 0, s + i + tl) & vm;
+#endif
         const uint64_t z = ~y & vm;
-        uint64_t yp = shfl_up64(y, 1);
-        if (lane == 0) yp = cnt ? ~0ull << (64 - cnt) : 0ull;
+        const uint64_t yp = wave_shr1_64(y, cnt ? ~0ull << (64 - cnt) : 0ull);  // lane 0: the carried run
         uint64_t a = y;
         for (uint32_t q = 1; q < L; ++q) a &= (y << q) | (yp >> (64 - q));
         const uint32_t zc = (uint32_t)__popcll(z);
-        uint32_t zin = zc;  // inclusive prefix of opposing pairs over lanes
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)zin, o);
-            if (lane >= (uint32_t)o) zin += v;
-        }
+        const uint32_t zin = wave_incl_sum(zc);  // inclusive prefix of opposing pairs over lanes
         const uint32_t zex = zin - zc;
-        uint64_t t0 = 0;  // restart offset in the window
-        uint32_t opp0 = opp;
-        bool carried = true;  // t0 = 0 with the carried run and count
-        for (;;) {
-            // run event: a run end at t >= thr (all its pairs at >= t0)
-            const uint64_t thr = carried ? 0 : t0 + L - 1;
-            const uint64_t am = thr <= tl ? a : (thr - tl >= 64 ? 0ull : a & (~0ull << (thr - tl)));
-            const uint64_t mr = __ballot(am != 0);
-            uint64_t tr = 4096;
-            if (mr) {
-                const uint32_t f = (uint32_t)__builtin_ctzll(mr);
-                tr = 64ull * f + (uint64_t)__builtin_ctzll(rdlane64(am, f));
+        // run event: the first run end at t >= thr (all its pairs at >= the
+        // restart); run ends are rare, so the answer is kept while thr has not
+        // passed it, and found from the lanes that hold any (mr) otherwise.
+        const uint64_t mr = __ballot(a != 0);
+        auto run_at = [&](uint64_t thr) -> uint64_t {
+            if (thr >= 4096) return 4096;
+            const uint32_t l = (uint32_t)(thr >> 6);
+            uint64_t m = mr & (~0ull << l);
+            while (m) {
+                const uint32_t f = (uint32_t)__builtin_ctzll(m);
+                uint64_t bits = rdlane64(a, f);
+                if (f == l) bits &= ~0ull << (thr & 63);
+                if (bits) return 64ull * f + (uint64_t)__builtin_ctzll(bits);
+                m &= m - 1;
             }
+            return 4096;
+        };
+        uint64_t tr = run_at(0);  // t0 = 0 with the carried run: thr 0
+        uint64_t t0 = 0;          // restart offset in the window
+        uint32_t opp0 = opp;
+        for (;;) {
             // jump event: the (TT - opp0)-th opposing pair at or after t0
             uint32_t before = 0;
             if (t0) {
@@ -1089,10 +1145,11 @@ __device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkPar
             const uint32_t target = before + (TT - opp0);
             const uint64_t mj = __ballot(zin >= target);
             uint64_t tj = 4096;
-            if (mj) {
+            if (mj) {  // select in lane f's word: lane j counts its bits 0..j (VALU, not a scalar bisection)
                 const uint32_t f = (uint32_t)__builtin_ctzll(mj);
                 const uint32_t need = target - (uint32_t)__builtin_amdgcn_readlane((int)zex, (int)f);
-                tj = 64ull * f + select_bit(rdlane64(z, f), need);
+                const uint64_t ms = __ballot((uint32_t)__popcll(rdlane64(z, f) & pmask) >= need);
+                tj = 64ull * f + (uint64_t)__builtin_ctzll(ms);
             }
             if (tr < tj) return i + tr + 1;  // (tr < lim: bits past the end are clear)
             if (tj >= 4096) {
@@ -1108,13 +1165,13 @@ __device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkPar
             // jump
             t0 = tj + J;
             opp0 = 0;
-            carried = false;
             if (t0 >= 4096 || t0 >= lim) {
                 i += t0;
                 cnt = 0;
                 opp = 0;
                 break;
             }
+            if (tr < t0 + L - 1) tr = run_at(t0 + L - 1);
         }
     }
     return end;
@@ -1158,7 +1215,7 @@ __global__ __launch_bounds__(256) void jtab_kernel(const StreamTable st, const W
     __shared__ __attribute__((aligned(16))) uint8_t res_lds[256 * kJSlot];
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
-    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), pc)) return;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + wave_id(), pc)) return;
     uint8_t *res = res_lds + threadIdx.x * kJSlot;
     const uint32_t si = pc.si;
     const uint64_t off = pc.off;
@@ -1333,7 +1390,7 @@ template <int kAlgo>
 __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
     constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + wave_id();
     if (g >= st.total_spans) return;
     uint32_t si;
     uint64_t off;
@@ -1343,7 +1400,7 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
     __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
     const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
-                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
+                lslot + (kAlgo == 5 ? wave_id() * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     const uint64_t *rs = wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t c = 0;
@@ -1361,13 +1418,34 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
     if (lane == 0) ws.E[g] = c;
     uint32_t cnt = 0;
     uint64_t *list = ws.list + g * wp.cap;
+    // Starts are held in lanes (lane j: list[cnt - nh + j]) and stored 64 at a
+    // time: the wave's next window load never waits behind a start's store
+    // (loads and stores share one counter on gfx9: a per-chunk store put an
+    // HBM write round trip into every chunk's step).
+    uint64_t held = 0;
+    uint32_t nh = 0;
+    auto flush = [&]() {
+        const uint32_t base = cnt - nh;
+        if (lane < nh && base + lane < wp.cap) list[base + lane] = held;
+        nh = 0;
+    };
     while (c < seg_end) {
-        if (lane == 0 && cnt < wp.cap) list[cnt] = c;
+        if (lane == nh) held = c;
+        ++nh;
         ++cnt;
+        if (nh == 64) flush();
         const uint64_t d = wcut<kAlgo>(B, c, len - c, wp, lane);
         c += d;
+        const uint32_t c0 = cnt;
         take_run<kAlgo>(B, rs, d, pk, c, len, seg_end, wp, lane, list, cnt);
+        if (cnt != c0 && nh) {  // a quiet run's starts went straight to the list
+            const uint32_t k = cnt;
+            cnt = c0;
+            flush();
+            cnt = k;
+        }
     }
+    flush();
     if (lane == 0) {
         ws.X[g] = c;
         ws.N[g] = cnt;
@@ -1513,7 +1591,7 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     if (round_stops(ws.gate)) return;  // the previous round settled everything (or went quiet)
     constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + wave_id();
     if (g >= st.total_spans) return;
     uint32_t si;
     uint64_t off;
@@ -1533,7 +1611,7 @@ __global__ __launch_bounds__(256) void wfix_kernel(const StreamTable st, const W
     __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
     const WBm B{wp.bm + st.span_base[si] * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
                 kAlgo == 5 ? wp.jt + st.span_base[si] * (uint64_t)wp.seg_words * 24 : nullptr,
-                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
+                lslot + (kAlgo == 5 ? wave_id() * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + st.span_base[si] * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     const uint64_t *rs = wp.rsum ? wp.rsum + st.span_base[si] * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t gg = g;
@@ -1639,14 +1717,14 @@ template <int kAlgo>
 __global__ __launch_bounds__(256) void wserial_kernel(const StreamTable st, const WalkParams wp, const WalkState ws) {
     constexpr uint32_t nbm = kAlgo == 4 ? 3 : kAlgo == 5 ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t si = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t si = (uint64_t)blockIdx.x * 4 + wave_id();
     if (si >= st.n) return;
     const uint64_t g0 = st.span_base[si], g1 = st.span_base[si + 1];
     const uint64_t len = st.lens[si];
     __shared__ __attribute__((aligned(16))) uint8_t lslot[kAlgo == 5 ? 4 * kLeapSlot : 16];
     const WBm B{wp.bm + g0 * (uint64_t)wp.seg_words * nbm, (len + 63) >> 6,
                 kAlgo == 5 ? wp.jt + g0 * (uint64_t)wp.seg_words * 24 : nullptr,
-                lslot + (kAlgo == 5 ? (threadIdx.x >> 6) * kLeapSlot : 0),
+                lslot + (kAlgo == 5 ? wave_id() * kLeapSlot : 0),
                 kAlgo == 5 ? wp.jt8 + g0 * (uint64_t)wp.seg_words / 8 * 24 : nullptr};
     const uint64_t *rs = wp.rsum ? wp.rsum + g0 * (uint64_t)wp.seg_words / 64 * kQuietKinds<kAlgo> : nullptr;
     uint64_t xprev = 0;
@@ -2050,7 +2128,7 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
-    if (!piece_of(st, wp, (uint64_t)blockIdx.x * kRabinWaves + (threadIdx.x >> 6), pc)) return;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * kRabinWaves + wave_id(), pc)) return;
     const uint32_t om = (lane & 15) * 8, oo = 128 + om;  // this lane's mod / out replica
     lds_wchar *tb = (lds_wchar *)rt;
     const uint64_t len = st.lens[pc.si];
@@ -2136,7 +2214,7 @@ __device__ __forceinline__ void ultra_load(uint4 (&v)[6], const uint8_t *base, u
 __global__ __launch_bounds__(256) void ubits_kernel(const StreamTable st, const WalkParams wp) {
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
-    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), pc)) return;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + wave_id(), pc)) return;
     const uint64_t off = pc.off;
     const uint64_t len = st.lens[pc.si];
     const uint8_t *base = st.ptrs[pc.si];
@@ -2179,7 +2257,7 @@ __global__ __launch_bounds__(256) void lbits_kernel(const StreamTable st, const 
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
-    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6), pc)) return;
+    if (!piece_of(st, wp, (uint64_t)blockIdx.x * 4 + wave_id(), pc)) return;
     const uint64_t *tl = lt + (lane & (kLeapReps - 1));
     const uint64_t len = st.lens[pc.si];
     const uint8_t *base = st.ptrs[pc.si];
@@ -2486,7 +2564,7 @@ bool bits_write_summary(const WalkParams &wp) {
 template <int kAlgo>
 __global__ __launch_bounds__(256) void qseg_kernel(const StreamTable st, const WalkParams wp) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + wave_id();
     if (g >= st.total_spans) return;
     uint32_t si;
     uint64_t off;
