@@ -247,8 +247,8 @@ int Engine::ensure_host_staging(size_t n) {
     const size_t want = n + 64;
     // ptrs[W] lens[W] span_base[W] tails[W] | stats ++ first[n+1] (fixed: first[n+1])
     // stream tables 4 n, device-written stats / flags ++ first[n+1] (n + 32),
-    // fix-up round flag blocks (4 x walk::kMaxFixRounds)
-    HIP_TRY(hipHostMalloc(&h_stage_, (5 * want + 32 + 4 * walk::kMaxFixRounds) * sizeof(uint64_t),
+    // the walk's flags[4] and fix-up round flag blocks (4 x walk::kMaxFixRounds)
+    HIP_TRY(hipHostMalloc(&h_stage_, (5 * want + 36 + 4 * walk::kMaxFixRounds) * sizeof(uint64_t),
                           hipHostMallocCoherent));
     h_stage_streams_ = want;
     return CDC_OK;
@@ -1011,10 +1011,12 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
 
 int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64_t *first, hipStream_t s) {
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_flags = h + 4 * h_stage_streams_;  // flags[4] ++ first[n+1]
-    uint64_t *h_first = h_flags + 4;
-    HIP_TRY(hipMemsetAsync(wst_.flags, 0, 4 * 8, s));
+    uint64_t *h_first = h + 4 * h_stage_streams_ + 4;  // first[n+1]
+    uint64_t *h_flags = h + 5 * h_stage_streams_ + 32;  // flags[4] ++ the round blocks, one copy
+    uint64_t *h_rf = h_flags + 4;
+    const uint32_t R = max_rounds_ < walk::kMaxFixRounds ? max_rounds_ : walk::kMaxFixRounds;
     HIP_TRY(hipEventRecord(ev_[0], s));
+    HIP_TRY(walk::launch_flags_init(wst_.flags, R, s));
     static const bool diag = std::getenv("CHUNKFS_AMD_WALKDIAG") != nullptr;  // phase times + candidates
     auto lap = [&](const char *what) -> int {
         if (!diag) return CDC_OK;
@@ -1052,14 +1054,13 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     // round r counts into its own flag block (rf + 4 r) and returns at once on
     // the device when round r-1 changed no exit (WalkState::gate), so the host
     // waits once per group instead of once per round.
+    // The output is queued right behind the first group, gated on the device
+    // by the same rule (walk::launch_emit's egate): when that group settles
+    // -- the common case -- the call needs one host wait, not two.
     constexpr uint32_t kGroup = 4;
     unsigned long long *rf = wst_.flags + 4;
-    uint64_t *h_rf = h + 5 * h_stage_streams_ + 32;
-    const uint32_t R = max_rounds_ < walk::kMaxFixRounds ? max_rounds_ : walk::kMaxFixRounds;
-    HIP_TRY(hipMemsetAsync(rf, 0, (size_t)R * 4 * 8, s));
-    HIP_TRY(hipMemset2DAsync(rf + 2, 32, 0xFF, 8, R, s));  // lowest segment whose exit changed
     uint64_t rewalked = 0, round_errors = 0;
-    bool settled = false, quiet_stop = false;
+    bool settled = false, quiet_stop = false, queued = false;
     uint32_t launched = 0, last_round = 0;
     while (launched < R && !settled) {
         const uint32_t end = launched + kGroup < R ? launched + kGroup : R;
@@ -1079,8 +1080,14 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
                              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
             }
         }
+        queued = launched == 0 && !diag;
         launched = end;
-        HIP_TRY(hipMemcpyAsync(h_rf, rf, (size_t)launched * 4 * 8, hipMemcpyDeviceToHost, s));
+        if (queued) {
+            HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s, rf, launched));
+            HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+        }
+        HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, (4 + (size_t)launched * 4) * 8, hipMemcpyDeviceToHost, s));
+        if (queued) HIP_TRY(hipEventRecord(ev_[2], s));
         HIP_TRY(hipStreamSynchronize(s));
         // The first round that settled everything, or whose changed exits
         // were mostly quiet-run re-walks (zero-filled / constant regions:
@@ -1120,11 +1127,13 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
     }
     (void)lap("fixup");
-    HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
-    HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(ev_[2], s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (!(queued && settled && launched <= kGroup)) {  // (else the gated output already ran)
+        HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
+        HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(ev_[2], s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     if (h_flags[1] + round_errors != 0) {
         set_error("segment walk: chunk list or output bound exceeded (internal error)");
         return CDC_EDEVICE;

@@ -1064,15 +1064,6 @@ __device__ __forceinline__ void take_run(const WBm &B, const uint64_t *rs, uint6
     pk = k ? kind : -1;
 }
 
-__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
-    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, o), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), o);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// The wave walks are issue-bound, not latency-bound: one scalar unit per CU
-// serves all 16 resident waves, so every restart's instruction count is paid
-// 16 times over (a scalar 64-bit select bisection was ~65 SALU instructions of
-// a restart's ~90; the lane-parallel select is 5 VALU + 2 SALU).
 // SeqCDC over bitmap 0 (pair p in the mode's direction), a window of 4096
 // positions per load (lane l on positions 64l .. 64l+63 of it).  From a
 // restart point t0 (the chunk's min, or a jump's landing) the rule is two
@@ -1083,29 +1074,27 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int o) {
 // carried from the previous window); the n-th opposing pair from a lane
 // prefix of popcounts and a select in the one lane that holds it.  Several
 // restarts per window are handled from the same registers.
+//
+// The walk's cost is that restart chain (~7 restarts per chunk on random
+// data; a timing build without jumps walked 1 GiB in 119 us instead of 365),
+// a dependent scalar sequence per restart, so each restart is kept short:
+// window offsets in 32 bits (one SALU compare each, where 64-bit unsigned
+// compares go through a VALU v_cmp and back), the select inside the lane by
+// all lanes at once (5 VALU + 2 SALU, was a ~65-instruction scalar
+// bisection), and the run event kept until the restart passes it.
 __device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkParams &wp, uint32_t lane) {
     if (n <= wp.min) return n;
     const uint64_t end = n < wp.max ? n : wp.max;
-#ifdef CDC_EXP_SEQ_NOJUMP  // (timing experiment: no jumps)
-    const uint32_t L = wp.seq_len, TT = 1u << 20, J = wp.seq_jump;
-#else
     const uint32_t L = wp.seq_len, TT = wp.seq_trig, J = wp.seq_jump;
-#endif
+    const uint32_t Jc = min(J, 1u << 30);  // (tj + Jc fits 32 bits; a larger jump leaves the window anyway)
     uint64_t i = wp.min;        // window start (relative to s)
     uint32_t cnt = 0, opp = 0;  // run / opposing pairs carried into the window
     const uint64_t pmask = lane == 63 ? ~0ull : (2ull << lane) - 1;
     while (i < end) {
-        const uint64_t lim = end - i;  // valid positions of the window: t < lim
-        const uint64_t tl = 64ull * lane;
+        const uint32_t lim = (uint32_t)min(end - i, (uint64_t)1 << 30);  // valid positions of the window: t < lim
+        const uint32_t tl = 64u * lane;
         const uint64_t vm = tl >= lim ? 0ull : (lim - tl >= 64 ? ~0ull : (1ull << (lim - tl)) - 1);
-#ifdef CDC_EXP_SEQ_NOLOAD  // (timing experiment: synthetic bits instead of the bitmap)
-        uint64_t hx = (s + i + tl) * 0x9E3779B97F4A7C15ull;
-        hx ^= hx >> 29;
-        hx *= 0xBF58476D1CE4E5B9ull;
-        const uint64_t y = (hx ^ (hx >> 32)) & vm;
-#else
         const uint64_t y = B.bits64(1, 0, s + i + tl) & vm;
-#endif
         const uint64_t z = ~y & vm;
         const uint64_t yp = wave_shr1_64(y, cnt ? ~0ull << (64 - cnt) : 0ull);  // lane 0: the carried run
         uint64_t a = y;
@@ -1117,39 +1106,39 @@ __device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkPar
         // restart); run ends are rare, so the answer is kept while thr has not
         // passed it, and found from the lanes that hold any (mr) otherwise.
         const uint64_t mr = __ballot(a != 0);
-        auto run_at = [&](uint64_t thr) -> uint64_t {
+        auto run_at = [&](uint32_t thr) -> uint32_t {
             if (thr >= 4096) return 4096;
-            const uint32_t l = (uint32_t)(thr >> 6);
+            const uint32_t l = thr >> 6;
             uint64_t m = mr & (~0ull << l);
             while (m) {
                 const uint32_t f = (uint32_t)__builtin_ctzll(m);
                 uint64_t bits = rdlane64(a, f);
                 if (f == l) bits &= ~0ull << (thr & 63);
-                if (bits) return 64ull * f + (uint64_t)__builtin_ctzll(bits);
+                if (bits) return 64u * f + (uint32_t)__builtin_ctzll(bits);
                 m &= m - 1;
             }
             return 4096;
         };
-        uint64_t tr = run_at(0);  // t0 = 0 with the carried run: thr 0
-        uint64_t t0 = 0;          // restart offset in the window
+        uint32_t tr = run_at(0);  // t0 = 0 with the carried run: thr 0
+        uint32_t t0 = 0;          // restart offset in the window
         uint32_t opp0 = opp;
         for (;;) {
             // jump event: the (TT - opp0)-th opposing pair at or after t0
             uint32_t before = 0;
             if (t0) {
-                const uint32_t l0 = (uint32_t)(t0 >> 6), b0 = (uint32_t)(t0 & 63);
+                const uint32_t l0 = t0 >> 6, b0 = t0 & 63;
                 const uint64_t zl = rdlane64(z, l0);
                 before = (uint32_t)__builtin_amdgcn_readlane((int)zex, (int)l0) +
                          (b0 ? (uint32_t)__popcll(zl & ((1ull << b0) - 1)) : 0u);
             }
             const uint32_t target = before + (TT - opp0);
             const uint64_t mj = __ballot(zin >= target);
-            uint64_t tj = 4096;
+            uint32_t tj = 4096;
             if (mj) {  // select in lane f's word: lane j counts its bits 0..j (VALU, not a scalar bisection)
                 const uint32_t f = (uint32_t)__builtin_ctzll(mj);
                 const uint32_t need = target - (uint32_t)__builtin_amdgcn_readlane((int)zex, (int)f);
                 const uint64_t ms = __ballot((uint32_t)__popcll(rdlane64(z, f) & pmask) >= need);
-                tj = 64ull * f + (uint64_t)__builtin_ctzll(ms);
+                tj = 64u * f + (uint32_t)__builtin_ctzll(ms);
             }
             if (tr < tj) return i + tr + 1;  // (tr < lim: bits past the end are clear)
             if (tj >= 4096) {
@@ -1157,20 +1146,21 @@ __device__ uint64_t wcut_seq(const WBm &B, uint64_t s, uint64_t n, const WalkPar
                 // no event in [t0, 4096): carry the run ending at 4095 and the count
                 const uint64_t y63 = rdlane64(y, 63);
                 const uint32_t r63 = ~y63 ? (uint32_t)__builtin_clzll(~y63) : 64u;
-                cnt = (uint32_t)min((uint64_t)r63, 4096 - t0);
+                cnt = min(r63, 4096u - t0);
                 opp = opp0 + ((uint32_t)__builtin_amdgcn_readlane((int)zin, 63) - before);
                 i += 4096;
                 break;
             }
             // jump
-            t0 = tj + J;
+            const uint32_t tn = tj + Jc;
             opp0 = 0;
-            if (t0 >= 4096 || t0 >= lim) {
-                i += t0;
+            if (tn >= 4096 || tn >= lim) {
+                i += (uint64_t)tj + J;
                 cnt = 0;
                 opp = 0;
                 break;
             }
+            t0 = tn;
             if (tr < t0 + L - 1) tr = run_at(t0 + L - 1);
         }
     }
@@ -2040,17 +2030,28 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
             cur = nxt;
         });
     } else if constexpr (kAlgo == 6) {
-        // SeqCDC: bit p = (b[p] > b[p-1]) (increasing) or (b[p] < b[p-1]).
-        uint32_t last = p0 >= 1 ? base[p0 - 1] : 0u;
+        // SeqCDC: bit p = (b[p] > b[p-1]) (increasing) or (b[p] < b[p-1]),
+        // four bytes per dword (SWAR): with x, y the bytes compared, bit 7 of
+        // t = (x | 0x80) - (y & 0x7F) - 1 is (x & 0x7F) > (y & 0x7F) (no
+        // borrow leaves a byte), and x > y takes x's bit 7 where bits 7
+        // differ, t's elsewhere; the four bit 7s gather into a nibble.
+        uint32_t lastw = p0 >= 1 ? (uint32_t)base[p0 - 1] << 24 : 0u;  // b[a-1] in bits 24..31
         uint64_t acc = 0, wlast = 0;
         for_chunks(base, len, p0, p1, [&](const uint4 &cur, uint64_t a) {
             const uint32_t sh = (uint32_t)((a - p0) & 63);
+            uint32_t b16 = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t b = byte_of(cur, j);
-                acc |= (uint64_t)(wp.seq_mode ? b < last : b > last) << (sh + j);
-                last = b;
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t W = word_of(cur, q);
+                const uint32_t P = __builtin_amdgcn_alignbit(W, lastw, 24);  // byte k: b[i + k - 1]
+                lastw = W;
+                const uint32_t x = wp.seq_mode ? P : W, y = wp.seq_mode ? W : P;
+                const uint32_t t = (x | 0x80808080u) - (y & 0x7F7F7F7Fu) - 0x01010101u;
+                const uint32_t d = x ^ y;
+                const uint32_t h = ((d & x) | (~d & t)) & 0x80808080u;
+                b16 |= ((((h >> 7) * 0x204081u) >> 21) & 0xFu) << (4 * q);
             }
+            acc |= (uint64_t)b16 << sh;
             if (sh == 48 || a + 16 >= p1) {
                 out[(a - p0) >> 6] = acc;
                 wlast = acc;
@@ -2473,7 +2474,23 @@ __device__ __forceinline__ uint64_t block_exclusive(uint64_t v, uint64_t *sh, ui
     return ex;
 }
 
-__global__ __launch_bounds__(kScanBlock) void sum_kernel(const StreamTable st, const WalkState ws) {
+// The output kernels queued behind the first group of fix-up rounds (egate:
+// its first flag block, egn rounds) run only when one of those rounds settled
+// every segment before any round handed off to the in-order pass -- the
+// host's rule in Engine::run_walk, which otherwise re-queues them.
+__device__ __forceinline__ bool emit_skips(const unsigned long long *egate, uint32_t egn) {
+    if (!egate) return false;
+    for (uint32_t r = 0; r < egn; ++r) {
+        const unsigned long long ch = egate[4 * r], q = egate[4 * r + 3] >> 32;
+        if (ch == 0) return false;
+        if (2 * q >= ch) return true;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(kScanBlock) void sum_kernel(const StreamTable st, const WalkState ws,
+                                                         const unsigned long long *egate, uint32_t egn) {
+    if (emit_skips(egate, egn)) return;
     __shared__ uint64_t sh[kScanBlock];
     const uint64_t g = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x;
     const uint64_t v = g < st.total_spans ? ws.N[g] : 0;
@@ -2483,7 +2500,9 @@ __global__ __launch_bounds__(kScanBlock) void sum_kernel(const StreamTable st, c
 }
 
 // One block: exclusive prefix of the nb block sums in place; bsum[nb] = total.
-__global__ __launch_bounds__(kScanBlock) void prefix_kernel(const WalkState ws, uint64_t nb) {
+__global__ __launch_bounds__(kScanBlock) void prefix_kernel(const WalkState ws, uint64_t nb,
+                                                            const unsigned long long *egate, uint32_t egn) {
+    if (emit_skips(egate, egn)) return;
     __shared__ uint64_t sh[kScanBlock];
     uint64_t carry = 0;
     for (uint64_t b0 = 0; b0 < nb; b0 += kScanBlock) {
@@ -2499,7 +2518,9 @@ __global__ __launch_bounds__(kScanBlock) void prefix_kernel(const WalkState ws, 
 
 __global__ __launch_bounds__(kScanBlock) void emit_kernel(const StreamTable st, const WalkParams wp,
                                                           const WalkState ws, cdc_chunk_pod *out,
-                                                          uint64_t out_cap) {
+                                                          uint64_t out_cap, const unsigned long long *egate,
+                                                          uint32_t egn) {
+    if (emit_skips(egate, egn)) return;
     __shared__ uint64_t sh[kScanBlock];
     const uint64_t g = (uint64_t)blockIdx.x * kScanBlock + threadIdx.x;
     const uint32_t n = g < st.total_spans ? ws.N[g] : 0;
@@ -2519,7 +2540,9 @@ __global__ __launch_bounds__(kScanBlock) void emit_kernel(const StreamTable st, 
     }
 }
 
-__global__ void first_kernel(const StreamTable st, const WalkState ws, uint64_t nb) {
+__global__ void first_kernel(const StreamTable st, const WalkState ws, uint64_t nb, const unsigned long long *egate,
+                             uint32_t egn) {
+    if (emit_skips(egate, egn)) return;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > st.n) return;
     const uint64_t g = i < st.n ? st.span_base[i] : st.total_spans;
@@ -2629,11 +2652,29 @@ hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkSt
     return dispatch(0, st, wp, ws, s);
 }
 
+// A round's snapshots, both arrays in one launch (skipped with the round).
+__global__ __launch_bounds__(256) void snap_kernel(const WalkState ws, uint64_t n) {
+    if (round_stops(ws.gate)) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        ws.Xs[i] = ws.X[i];
+        ws.Es[i] = ws.E[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void flags_init_kernel(unsigned long long *flags, uint32_t rounds) {
+    for (uint32_t i = threadIdx.x; i < 4 + 4 * rounds; i += 256) flags[i] = i >= 4 && (i & 3) == 2 ? ~0ull : 0ull;
+}
+
+hipError_t launch_flags_init(unsigned long long *flags, uint32_t rounds, hipStream_t s) {
+    flags_init_kernel<<<1, 256, 0, s>>>(flags, rounds);
+    return hipGetLastError();
+}
+
 hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
-    hipError_t e = hipMemcpyAsync(ws.Xs, ws.X, st.total_spans * 8, hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(ws.Es, ws.E, st.total_spans * 8, hipMemcpyDeviceToDevice, s);
+    const uint64_t sb = (st.total_spans + 255) / 256;
+    snap_kernel<<<(unsigned)(sb < 1024 ? sb : 1024), 256, 0, s>>>(ws, st.total_spans);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (wp.wave && wp.nbm) {
         const unsigned blocks = (unsigned)((st.total_spans + 3) / 4);
@@ -2659,15 +2700,15 @@ hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const Walk
 }
 
 hipError_t launch_emit(const StreamTable &st, const WalkParams &wp, const WalkState &ws, void *d_out,
-                       uint64_t out_cap, hipStream_t s) {
+                       uint64_t out_cap, hipStream_t s, const unsigned long long *egate, uint32_t egn) {
     const uint64_t nb = (st.total_spans + kScanBlock - 1) / kScanBlock;
     if (nb) {
-        sum_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, ws);
-        prefix_kernel<<<1, kScanBlock, 0, s>>>(ws, nb);
+        sum_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, ws, egate, egn);
+        prefix_kernel<<<1, kScanBlock, 0, s>>>(ws, nb, egate, egn);
         emit_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, wp, ws, reinterpret_cast<cdc_chunk_pod *>(d_out),
-                                                        out_cap);
+                                                        out_cap, egate, egn);
     }
-    first_kernel<<<(unsigned)((st.n + 1 + 255) / 256), 256, 0, s>>>(st, ws, nb);
+    first_kernel<<<(unsigned)((st.n + 1 + 255) / 256), 256, 0, s>>>(st, ws, nb, egate, egn);
     return hipGetLastError();
 }
 

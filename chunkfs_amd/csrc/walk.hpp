@@ -115,18 +115,25 @@ constexpr int kScanBlock = 256;  // prefix / emit block (segments per block)
 // summary (wp.rsum may be non-null only then).
 bool bits_write_summary(const WalkParams &wp);
 hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t s);
+// Zeroes the main flag block and the `rounds` round blocks after it (their
+// word 2, the lowest changed segment, to ~0): one launch instead of three fills.
+hipError_t launch_flags_init(unsigned long long *flags, uint32_t rounds, hipStream_t s);
 // Link mode: candidate lists (wave per segment), then the links (lane per candidate).
 hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t s);
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
-// One Jacobi round: snapshot X, then re-walk every segment whose entry is not
+// One Jacobi round: snapshot X and E (one launch), then re-walk every segment whose entry is not
 // its predecessor's exit, stopping where the new chain meets the old one.
 // flags[0] counts the re-walks that changed an exit (the host loops while > 0).
 hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
 // Exact in-order pass over all segments from the lowest one re-walked.
 hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
-// Prefix of N, first[], and the Chunk{offset,length} output.
+// Prefix of N, first[], and the Chunk{offset,length} output.  egate (the
+// first of egate_rounds round flag blocks) non-null: every kernel returns at
+// once unless those rounds settled (the host's rule, run_walk), so the output
+// can be queued behind the first group of rounds without a host round trip.
 hipError_t launch_emit(const StreamTable &st, const WalkParams &wp, const WalkState &ws, void *d_out,
-                       uint64_t out_cap, hipStream_t s);
+                       uint64_t out_cap, hipStream_t s, const unsigned long long *egate = nullptr,
+                       uint32_t egate_rounds = 0);
 
 }  // namespace walk
 }  // namespace cdc
