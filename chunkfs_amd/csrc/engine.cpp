@@ -1057,13 +1057,17 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     // The output is queued right behind the first group, gated on the device
     // by the same rule (walk::launch_emit's egate): when that group settles
     // -- the common case -- the call needs one host wait, not two.
+    // The first group is one round: on random data the first round settles
+    // every segment (its re-walks meet the old chains), and the gated no-op
+    // rounds after it cost ~14 us each (snapshot + fix launches).
     constexpr uint32_t kGroup = 4;
     unsigned long long *rf = wst_.flags + 4;
     uint64_t rewalked = 0, round_errors = 0;
     bool settled = false, quiet_stop = false, queued = false;
     uint32_t launched = 0, last_round = 0;
     while (launched < R && !settled) {
-        const uint32_t end = launched + kGroup < R ? launched + kGroup : R;
+        const uint32_t grp = launched == 0 ? 1u : kGroup;
+        const uint32_t end = launched + grp < R ? launched + grp : R;
         for (uint32_t r = launched; r < end; ++r) {
             // Plain Jacobi for the first ahead_after_ rounds, then run-ahead
             // re-walks (walk.hip fix_kernel) so long non-merging stretches
@@ -1127,7 +1131,7 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
     }
     (void)lap("fixup");
-    if (!(queued && settled && launched <= kGroup)) {  // (else the gated output already ran)
+    if (!(queued && settled && launched == 1)) {  // (else the gated output already ran)
         HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
         HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
