@@ -113,7 +113,9 @@ const char *cdc_last_error(void);
 
 /* Install a 256-entry GEAR table (fastcdc v2020 `GEAR`) for FastCDC handles.
  * The built-in table is a placeholder (include/chunkfs_amd_tables.h); a
- * maintainer pins parity with the Rust crate by passing the crate's table. */
+ * maintainer pins parity with the Rust crate by passing the crate's table.
+ * CDC_EINVAL while a streaming write (cdc_write_begin) is in progress on the
+ * handle: one write never mixes two tables. */
 int cdc_set_gear(cdc_handle_t *h, const uint64_t gear[256]);
 
 /* Install the Rabin polynomial of a CDC_ALGO_RABIN handle (the reference's
@@ -121,7 +123,8 @@ int cdc_set_gear(cdc_handle_t *h, const uint64_t gear[256]);
  * polynomial is absent offline, include/chunkfs_amd_cdc_params.h holds a
  * stand-in).  Degree 9..56 (the 48-byte window digest shifted by a byte stays
  * inside 64 bits); the tables are rebuilt for the handle.  CDC_EINVAL for
- * another algorithm or degree. */
+ * another algorithm or degree, and while a streaming write is in progress on
+ * the handle (one write never mixes two polynomials). */
 int cdc_set_rabin_poly(cdc_handle_t *h, uint64_t poly);
 
 /* ---- Device-resident batch API (configs 2, 4, 5: inputs already in HBM) --

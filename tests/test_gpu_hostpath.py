@@ -138,6 +138,8 @@ def test_stream_write_begin_twice_and_failure_rules():
         c.StreamWriter(ch)
     with pytest.raises(c.CdcError):
         c.write_spans(ch, data)  # cdc_fs_write also begins a write
+    with pytest.raises(c.CdcError):
+        ch.set_gear(np.arange(256, dtype=np.uint64))  # no table swap inside a write
     w.write(data[1 << 20:])
     spans, _ = w.finish()
     ref = _whole("fast", data)
@@ -147,6 +149,18 @@ def test_stream_write_begin_twice_and_failure_rules():
     spans2, _ = c.write_spans(ch, data)  # the handle is free again
     assert (spans2 == ref).all()
     ch.close()
+    # a Rabin handle refuses a new polynomial while its write is open
+    rb = _chunker("rabin")
+    w = c.StreamWriter(rb)
+    w.write(data[:1 << 20])
+    with pytest.raises(c.CdcError):
+        rb.set_poly(0x3DA3358B4DC173)
+    w.write(data[1 << 20:])
+    spans, _ = w.finish()
+    ref = _whole("rabin", data)
+    assert spans.shape == ref.shape and (spans == ref).all()
+    rb.set_poly(0x3DA3358B4DC173)  # free again
+    rb.close()
 
 
 def test_stream_write_edge_cases():
