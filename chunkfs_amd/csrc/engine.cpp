@@ -278,9 +278,6 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     const uint64_t nb = p3::resolve_blocks(S) + 2;
     const size_t o_stats = take(p3::kStatWords * 8), o_desc = take(6 * nb * 8);
     const size_t o_tails = take(N * 8);
-    // the scan's record links (span_links); done / lvalid generation words
-    const size_t o_ldist = take(S * cap * 4), o_ltgt = take(S * cap * 2), o_vcnt = take(S * 4);
-    const size_t o_vent = take(S * p3::kVirtSpan * 16), o_flags = take(2 * S * 4);
     (void)hipFree(ws_);
     ws_ = nullptr;
     ws_spans_ = 0;
@@ -305,13 +302,6 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     rs3_ = p3::Resolve{desc, desc + nb, desc + 2 * nb, desc + 3 * nb, desc + 4 * nb, desc + 5 * nb, 0};
     HIP_TRY(hipMemset(desc, 0, 6 * nb * 8));  // no stale status word can carry a live generation
     d_tails_ = reinterpret_cast<uint64_t *>(b + o_tails);
-    lk3_.ldist = reinterpret_cast<uint32_t *>(b + o_ldist);
-    lk3_.ltgt = reinterpret_cast<uint16_t *>(b + o_ltgt);
-    lk3_.vcnt = reinterpret_cast<uint32_t *>(b + o_vcnt);
-    lk3_.vent = reinterpret_cast<uint4 *>(b + o_vent);
-    lk3_.done = reinterpret_cast<uint32_t *>(b + o_flags);
-    lk3_.lvalid = lk3_.done + S;
-    HIP_TRY(hipMemset(lk3_.done, 0, 2 * S * 4));  // no stale word can carry a live generation
     return CDC_OK;
 }
 
@@ -441,14 +431,11 @@ int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
     h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the last resolve block
     p3::Resolve rs = rs3_;
     rs.gen = ++res_gen_;
-    p3::Links lk = lk3_;
-    lk.gen = (uint32_t)rs.gen;
-    if (lk.gen == 0) lk.gen = (uint32_t)(rs.gen = ++res_gen_);  // (never 0: the zeroed words' value)
     hipEvent_t *ev = tev_[fast_batches_ % kTimeRing];
     HIP_TRY(hipEventRecord(ev[0], s));
-    HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, lk, cp, cur_tails_, n_tails_, num_cus_, s));
+    HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, cur_tails_, n_tails_, num_cus_, s));
     HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, lk, ch3_, cp, rs, d_out, out_cap_, s));
+    HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, ch3_, cp, rs, d_out, out_cap_, s));
     HIP_TRY(hipEventRecord(ev[2], s));
     ++fast_batches_;
     // The resolve's last block writes the done word into coherent pinned

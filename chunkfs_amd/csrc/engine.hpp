@@ -189,7 +189,6 @@ class Engine {
     p3::Chains ch3_{};             // chunk starts spilled past the resolve's LDS
     p3::Compact cp3_{};
     p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
-    p3::Links lk3_{};              // record links made by the scan (generation-tagged, never re-zeroed)
     uint64_t res_gen_ = 0;
     uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids
     const uint64_t *cur_tails_ = nullptr;  // this batch's: d_tails_ or the staging block's

@@ -448,17 +448,6 @@ __device__ __noinline__ uint32_t scan_trunc(const uint8_t *base, uint32_t c, uin
 
 #endif
 
-// Write-through (sc1) 4-byte stores and loads: the records of a span are read
-// by another wave of the same launch (the link pass below) after a done word
-// (MI355X_MICROARCH.md "inter-workgroup visibility", Guideline 16 R1).
-typedef __attribute__((address_space(1))) uint32_t g_u32w;
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
-    return __hip_atomic_load((g_u32w *)const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
-    __hip_atomic_store((g_u32w *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Flush of one span: exact mask_s / mask_l flags for each hitting quarter
 // (re-hashed from the hash before it), each record's truncated-region result
 // (scan_trunc), position order, HBM write.  avail = stream bytes from the span
@@ -470,7 +459,7 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
     wave_sync_lds();
     uint32_t *cpos = cand.pos + g * cand.cap;
     if (ne > kEntCap) {  // too many hits for the LDS list: resolve takes the exact slow path
-        if (lane == 0) st_sc1(cand.count + g, cand.cap + 1);
+        if (lane == 0) cand.count[g] = cand.cap + 1;
         wave_sync_lds();
         return;
     }
@@ -519,222 +508,13 @@ __device__ __forceinline__ void flush_span(uint64_t g, const uint8_t *base, uint
                            fp.mask_s_sh, fp.mask_l_sh);
 #endif
             if (slot < cand.cap)
-                st_sc1(cpos + slot,
-                       (my_pos + j) | (t << kRecTShift) | (((hs >> j) & 1u) << 31) | (((hl >> j) & 1u) << 30));
+                cpos[slot] = (my_pos + j) | (t << kRecTShift) | (((hs >> j) & 1u) << 31) | (((hl >> j) & 1u) << 30);
             ++slot;
         }
     }
-    if (lane == 0) st_sc1(cand.count + g, total);
+    if (lane == 0) cand.count[g] = total;
     wave_sync_lds();
 }
-
-// ---- links in the scan -------------------------------------------------------
-//
-// The resolve's per-record work -- the link of every candidate record, the
-// next chunk start after a chunk starting there -- done by the scan's
-// persistent waves between spans, where its latency hides under the other
-// waves' hashing (the resolve kernel spent ~27 us per GiB on it after the
-// scan: profiles/r05a_diag.log).  Wave per span, one round after the span was
-// scanned: the span's records and the next span's (written through by a
-// sibling wave and published by its done word) in an LDS list; lane per
-// record: the truncated-region test from the bytes (47 lookups in the scan's
-// own replicated table), else the first qualifying record by a linear search
-// of the list, else the max / end cut.  Next starts that are
-// not records become the span's virtual entries, whose links are computed the
-// same way (three levels).  Anything out of reach -- a search past the next
-// span, a full virtual table, a poll timeout, an overflowed record list --
-// stays unknown (0), and the resolve computes it exactly as before.
-constexpr uint32_t kP1List = 512;             // records of a span and of the next one
-constexpr uint32_t kListPos = 0x0FFFFFFFu;    // list entry: position from the span start | hit flags
-constexpr uint32_t kP1Spin = 1u << 20;        // done-word poll bound (then: links unknown)
-constexpr uint32_t kDiagNoScanLinks = 2048;   // CHUNKFS_AMD_DIAG bit 11: no links in the scan (A/B)
-
-struct P1Scratch {                 // in the wave's transpose tile, free between spans
-    uint32_t list[kP1List];
-    uint32_t vpos[kVirtSpan];      // virtual entries: position from the span start
-    uint32_t vsrc[kVirtSpan];      // list index their search starts from
-    uint32_t vdist[kVirtSpan];
-    uint32_t vtgt[kVirtSpan];
-};
-
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-
-// Link of a chunk starting at list-relative offset crel (stream offset
-// off + crel), out of line (one copy of the truncated test in the scan's code:
-// an inlined copy per call site pushed the scan kernel's hot loop out of the
-// instruction cache).  The truncated test uses the scan's pre-shifted,
-// replicated LDS table (as trunc_words); the search starts at list entry k0.
-// Returns dist (bits 0-31; 0 = unknown) | target (bits 32-47) | bit 48: the
-// next start is a new virtual entry at crel + dist.
-__device__ __noinline__ uint64_t p1_link(uint32_t crel, uint32_t k0, uint64_t off, uint64_t n, const uint8_t *data,
-                                         uint64_t cover, uint32_t mn, uint32_t avg, uint32_t mx, uint32_t trunc,
-                                         uint64_t mask_s, uint64_t mask_l, const lds_u32 *list, uint32_t nl,
-                                         uint32_t c0, const lds_u64 *ltab, uint32_t rep) {
-    const uint64_t c = off + crel;
-    if (n - c <= mn) return (uint64_t)kTgtEnd << 32 | (uint32_t)(n - c);  // tail chunk
-    uint64_t rem = n - c, center = avg;
-    if (rem > mx) rem = mx; else if (rem < center) center = rem;
-    const uint64_t a0 = (mn / 2) * 2, ce = (center / 2) * 2, re = (rem / 2) * 2;
-    const uint64_t tl = min(a0 + (uint64_t)trunc, re);
-    uint64_t nx = c + rem;
-    bool found = false;
-    if (tl > a0) {  // the truncated region, from the bytes
-        const uint32_t len = (uint32_t)(tl - a0);
-        const uint64_t w0 = c + a0;
-        const uint32_t ns = ce > a0 ? (uint32_t)min(ce - a0, (uint64_t)64) : 0u;  // d < ns: mask_s
-        uint64_t h = 0, hits = 0;
-        if ((w0 & ~3ull) + 52 <= n) {
-            const uint64_t al = w0 & ~3ull;
-            const uint32_t sh = (uint32_t)(w0 - al);
-            uint32_t w[13];
-#pragma unroll
-            for (int i = 0; i < 13; ++i) w[i] = *(g_u32 *)(data + al + 4 * i);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) {
-                const uint32_t a = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t d = 4 * k + j;
-                    if (d >= kTruncMax) break;
-                    const uint32_t addr = __builtin_amdgcn_perm(rep, a, 0x0c0c0004u | ((uint32_t)j << 8));
-                    h = shl1_add(h, *reinterpret_cast<const lds_u64 *>(reinterpret_cast<lds_char *>(ltab) + addr));
-                    hits |= (uint64_t)((h & (d < ns ? mask_s : mask_l)) == 0) << d;
-                }
-            }
-        } else {  // near the stream end: bytes one at a time (positions >= n are never tested)
-            g_u8 *gb = as_global1(data);
-            for (uint32_t d = 0; d < len; ++d) {
-                h = (h << 1) + ltab[(uint32_t)gb[w0 + d] * kCopies + (rep >> 3)];
-                hits |= (uint64_t)((h & (d < ns ? mask_s : mask_l)) == 0) << d;
-            }
-        }
-        if (len < 64) hits &= (1ull << len) - 1;
-        if (hits) nx = w0 + (uint64_t)__builtin_ctzll(hits);
-        found = hits != 0;
-    }
-    if (!found && tl < re) {  // the first qualifying record
-        if (c + re > cover) return (uint64_t)kTgtNone << 32;  // records past the list: unknown
-        const uint32_t lo = crel + (uint32_t)tl, hi = crel + (uint32_t)re, cm = crel + (uint32_t)ce;
-        for (uint32_t k = k0; k < nl; ++k) {
-            const uint32_t r = list[k];
-            const uint32_t p = r & kListPos;
-            if (p >= hi) break;
-            if (p >= lo && (r & (p < cm ? kCandHitS : kCandHitL))) {
-                const uint32_t t = k < c0 ? k : (1u << kTgtDeltaShift) | (k - c0);
-                return (uint64_t)t << 32 | (p - crel);
-            }
-        }
-    }
-    const uint32_t dist = (uint32_t)(nx - c);
-    if (nx >= n) return (uint64_t)kTgtEnd << 32 | dist;
-    return 1ull << 48 | (uint64_t)kTgtNone << 32 | dist;
-}
-
-// The links of span g (stream si, stream offset off), wave-synchronous.
-__device__ __forceinline__ void span_links(const StreamTable &st, const FastParams &fp, const Candidates &cand,
-                                           const Links &lk, const uint64_t *tab, uint32_t rep, uint64_t g,
-                                           uint32_t si, uint64_t off, uint32_t lane, P1Scratch &S) {
-    const uint64_t n = st.lens[si];
-    const uint8_t *data = st.ptrs[si];
-    const uint64_t span = 1ull << st.span_log2;
-    const uint32_t cap = cand.cap;
-    const uint32_t c0 = ld_sc1(cand.count + g);
-    if (c0 > cap) return;  // overflowed: the resolve's exact path
-    const uint64_t end_g = min(off + span, n);
-    uint64_t cover = n;  // every record below this stream offset is in the list
-    uint32_t c1 = 0;
-    if (end_g < n) {  // the next span is this stream's: its records once stored
-        cover = end_g;
-        bool ok = false;
-        for (uint32_t k = 0; k < kP1Spin; ++k) {
-            if (ld_sc1(lk.done + g + 1) == lk.gen) {
-                ok = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: sc1 loads stay below)
-        if (ok) {
-            const uint32_t c = ld_sc1(cand.count + g + 1);
-            if (c <= cap && c0 + c <= kP1List) {
-                c1 = c;
-                cover = min(end_g + span, n);
-            }
-        }
-    }
-    for (uint32_t k = lane; k < c0; k += 64)
-        S.list[k] = ld_sc1(cand.pos + g * cap + k) & (kCandPosMask | kCandHitS | kCandHitL);
-    for (uint32_t k = lane; k < c1; k += 64) {
-        const uint32_t r = ld_sc1(cand.pos + (g + 1) * cap + k);
-        S.list[c0 + k] = ((r & kCandPosMask) + (uint32_t)span) | (r & (kCandHitS | kCandHitL));
-    }
-    wave_sync_lds();
-    const uint32_t nl = c0 + c1;
-    const lds_u32 *list = (const lds_u32 *)(S.list);
-    const lds_u64 *ltab = (const lds_u64 *)tab;
-    auto link = [&](uint32_t crel, uint32_t k0) {
-        return p1_link(crel, k0, off, n, data, cover, fp.min, fp.avg, fp.max, fp.trunc, fp.mask_s_sh, fp.mask_l_sh,
-                       list, nl, c0, ltab, rep);
-    };
-    uint32_t nv = 0;  // virtual entries requested (wave-uniform)
-    auto virt_slot = [&](bool mk) {
-        const uint64_t m = __ballot(mk);
-        const uint32_t v = nv + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        nv += (uint32_t)__popcll(m);
-        return v;
-    };
-    for (uint32_t b0 = 0; b0 < c0; b0 += 64) {
-        const uint32_t i = b0 + lane;
-        const uint64_t r = i < c0 ? link(S.list[i] & kListPos, i + 1) : (uint64_t)kTgtNone << 32;
-        const bool mkv = (r >> 48) & 1;
-        uint32_t tgt = (uint32_t)(r >> 32) & 0xFFFF;
-        const uint32_t v = virt_slot(mkv);
-        if (mkv && v < kVirtSpan) {
-            S.vpos[v] = (S.list[i] & kListPos) + (uint32_t)r;
-            S.vsrc[v] = i + 1;
-            tgt = kTgtVirt | v;
-        }
-        if (i < c0) {
-            lk.ldist[g * cap + i] = (uint32_t)r;
-            lk.ltgt[g * cap + i] = (uint16_t)tgt;
-        }
-    }
-    uint32_t v0 = 0;
-    for (int lvl = 0; lvl < 3; ++lvl) {  // virtual entries, level by level (<= 16: one batch)
-        const uint32_t v1 = min(nv, kVirtSpan);
-        if (v0 >= v1) break;
-        wave_sync_lds();
-        const uint32_t v = v0 + lane;
-        const uint64_t r = v < v1 ? link(S.vpos[v], S.vsrc[v]) : (uint64_t)kTgtNone << 32;
-        const bool mkv = (r >> 48) & 1;
-        uint32_t tgt = (uint32_t)(r >> 32) & 0xFFFF;
-        const uint32_t w = virt_slot(mkv);
-        if (mkv && w < kVirtSpan) {
-            S.vpos[w] = S.vpos[v] + (uint32_t)r;
-            S.vsrc[w] = S.vsrc[v];
-            tgt = kTgtVirt | w;
-        }
-        if (v < v1) {
-            S.vdist[v] = (uint32_t)r;
-            S.vtgt[v] = tgt;
-        }
-        v0 = v1;
-    }
-    const uint32_t nvt = min(nv, kVirtSpan);
-    wave_sync_lds();
-    if (lane < nvt) {
-        const bool done = lane < v0;  // entries of the last level have no link yet
-        lk.vent[g * kVirtSpan + lane] = make_uint4(S.vpos[lane], done ? S.vdist[lane] : 0u,
-                                                   done ? S.vtgt[lane] : (uint32_t)kTgtNone, 0u);
-    }
-    if (lane == 0) {
-        lk.vcnt[g] = nvt;
-        lk.lvalid[g] = lk.gen;  // (read by the resolve kernel: the launch boundary orders it)
-    }
-    wave_sync_lds();
-}
-
-static_assert(sizeof(P1Scratch) <= sizeof(uint4) * 64 * 5, "span_links scratch must fit a transpose tile");
 
 template <int kW>
 struct ScanLds {
@@ -753,8 +533,7 @@ struct ScanLds {
 template <bool kAlign, int kW, int kLook, int kMode>
 __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, const FastParams fp,
                                                            const uint64_t *__restrict__ gear,
-                                                           const Candidates cand, const Links lk,
-                                                           const Compact cp) {
+                                                           const Candidates cand, const Compact cp) {
     __shared__ ScanLds<kW> L;
     const uint64_t *tab = L.tab;
     for (int i = threadIdx.x; i < 256 * kCopies; i += kW * 64)
@@ -795,12 +574,6 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
     Q4 A, B, C;
     uint32_t si, wb = 0;
     uint64_t off;
-    // Links in the scan (span_links): the previous span's, pending.
-    const bool links = kMode == 0 && !(fp.diag & kDiagNoScanLinks);
-    P1Scratch &S1 = *reinterpret_cast<P1Scratch *>(&L.stage[wave][0]);
-    bool pend = false;
-    uint64_t pg = 0, poff = 0;
-    uint32_t psi = 0;
     uint64_t g = next_full((uint64_t)blockIdx.x * kW + wave, si, off);
     const uint8_t *base = nullptr, *gp = nullptr;
     auto prefetch = [&]() {  // first two steps and the carry bytes of span g
@@ -856,7 +629,6 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
 #undef CDC_PROC
         // This span's carry-in bytes and identity, then the next span's prefetch.
         const uint64_t g_cur = g, off_cur = off;
-        const uint32_t si_cur = si;
         const uint64_t avail_cur = st.lens[si] - off;
         const uint32_t wb_cur = wb;
         const uint8_t *base_cur = base;
@@ -875,23 +647,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
             append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, (lo + 32) | kEntFix, h0, ne, E);
         }
         flush_span(g_cur, base_cur, (uint32_t)span, avail_cur, sub - 1, ne, E, tab, rep, fp, cand, lane);
-        if constexpr (kMode == 0) {
-            if (links) {
-                // Publish the span's records (written through by the flush),
-                // then the links of the previous span: its successor, scanned by
-                // a sibling wave in the same round, is long stored.
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) st_sc1(lk.done + g_cur, lk.gen);
-                if (pend && !(fp.diag & 4096)) span_links(st, fp, cand, lk, tab, rep, pg, psi, poff, lane, S1);
-                pend = true;
-                pg = g_cur;
-                psi = si_cur;
-                poff = off_cur;
-            }
-        }
     }
-    // The last span's links: its successor is being scanned right now.
-    if (pend && !(fp.diag & 4096)) span_links(st, fp, cand, lk, tab, rep, pg, psi, poff, lane, S1);
 }
 
 // ---- scan, LDS-DMA input landing (A/B path: CHUNKFS_AMD_DIAG bit 10) ---------
@@ -1178,10 +934,9 @@ __global__ __launch_bounds__(kDmaW * 64, 1) void scan_dma_kernel(const StreamTab
 template <bool kAlign>
 __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, const FastParams fp,
                                                        const uint64_t *__restrict__ gear, const Candidates cand,
-                                                       const Links lk, const uint64_t *__restrict__ tails) {
+                                                       const uint64_t *__restrict__ tails) {
     __shared__ uint64_t tab[256 * kCopies];
     __shared__ uint32_t e_pos[kEntCap], e_hlo[kEntCap], e_hhi[kEntCap], e_cnt[kEntCap];
-    __shared__ P1Scratch p1;
     for (int i = threadIdx.x; i < 256 * kCopies; i += 64) tab[i] = gear[i / kCopies] << fp.tshift;
     __syncthreads();
     const uint32_t lane = threadIdx.x;
@@ -1212,11 +967,6 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
         append_hits(hit, p | kEntFix, h0, ne, E);
     }
     flush_span(g, base, span_len, span_len, 0, ne, E, tab, rep, fp, cand, lane);
-    // Its records for the main scan's link pass of the span before (which
-    // runs in the next launch), then its own links (it ends its stream).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) st_sc1(lk.done + g, lk.gen);
-    if (!(fp.diag & kDiagNoScanLinks)) span_links(st, fp, cand, lk, tab, rep, g, si, off, lane, p1);
 }
 
 
@@ -1469,10 +1219,7 @@ struct ChainWin {
     uint32_t scnt[kWinSlots];         // its records (> cap: overflowed)
     uint32_t pre[kWinSlots + 1];      // compact start of each slot's records
     uint32_t wpre[kWalkSpans + 1];    // output: chunk prefix of the walked spans
-    uint32_t vcn[kWinSlots];          // the scan's virtual entries of each slot (loaded)
-    uint32_t vbs[kWinSlots];          // their first window virtual index
-    uint8_t lval[kWinSlots];          // 1: the slot's links come from the scan (span_links)
-    uint32_t nrec, nvirt, nv0;
+    uint32_t nrec, nvirt;
 };
 
 struct BlockState {
@@ -1654,16 +1401,13 @@ __device__ __forceinline__ LinkItem link_item(const ChainWin &W, const FastParam
     it.known = kTruncUnknown;
     it.act = x < e1;
     if (!it.act) return it;
-    it.e = virt ? kWinRecs + x : x;
-    if (W.link[it.e] != 0) {  // loaded from the scan's link pass
-        it.act = false;
-        return it;
-    }
     if (virt) {
+        it.e = kWinRecs + x;
         it.j = W.vslot[x];
         it.c = W.vpos[x];
         it.i0 = win_lower(W, skey(W.ssi[it.j]) | it.c);
     } else {
+        it.e = x;
         it.j = W.rslot[x];
         it.c = W.key[x] & kKeyPos;
         it.i0 = x + 1;
@@ -1748,19 +1492,6 @@ __device__ __forceinline__ void item_link(ChainWin &W, const FastParams &fp, con
         lr = kWinRecs + v + 1;
     }
     if (it.act) W.lrec[it.e] = (uint16_t)lr;
-}
-
-// Window entry index + 1 of a link target of the scan's link pass (slot j's
-// record or virtual entry; 0: no entry, the walk then steps from the bytes).
-__device__ __forceinline__ uint16_t tgt_entry(const ChainWin &W, uint32_t t, int j) {
-    if (t == kTgtEnd || t == kTgtNone) return 0;
-    if (t & kTgtVirt) {
-        const uint32_t v = t & ~(uint32_t)kTgtVirt;
-        return v < W.vcn[j] ? (uint16_t)(kWinRecs + W.vbs[j] + v + 1) : (uint16_t)0;
-    }
-    const int jj = j + (int)(t >> kTgtDeltaShift);
-    const uint32_t idx = t & ((1u << kTgtDeltaShift) - 1);
-    return (jj < kWinSlots && idx < W.scnt[jj]) ? (uint16_t)(W.pre[jj] + idx + 1) : (uint16_t)0;
 }
 
 // Inter-block words (MI355X_MICROARCH.md "inter-workgroup visibility"; the
@@ -1938,7 +1669,7 @@ __device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) {
 #endif
 __global__ __launch_bounds__(kResThreads, CDC_RES_MINW) void resolve_kernel(const StreamTable st, const FastParams fp,
                                                               const uint64_t *__restrict__ gear,
-                                                              const Candidates cand, const Links lk, const Chains ch,
+                                                              const Candidates cand, const Chains ch,
                                                               const Compact cp, const Resolve rs,
                                                               cdc_chunk_pod *out, uint64_t out_cap) {
     __shared__ uint64_t tab[256];
@@ -1973,44 +1704,34 @@ __global__ __launch_bounds__(kResThreads, CDC_RES_MINW) void resolve_kernel(cons
         // 1. window metadata, then every record of the window (one batch of loads)
         if (lane < kWinSlots) {
             const int64_t g = gfirst + lane;
-            uint32_t si = ~0u, c = 0, vc = 0;
+            uint32_t si = ~0u, c = 0;
             uint64_t off = 0, n = 0;
             const uint8_t *p = nullptr;
-            bool lv = false;
             if (g >= 0 && (uint64_t)g < st.total_spans) {
                 locate(st, (uint64_t)g, si, off);
                 c = cand.count[g];
                 n = st.lens[si];
                 p = st.ptrs[si];
-                lv = lk.lvalid[g] == lk.gen;
-                vc = lv ? min(lk.vcnt[g], kVirtSpan) : 0u;
             }
             W.ssi[lane] = si;
             W.soff[lane] = off;
             W.scnt[lane] = c;
             W.slen[lane] = n;
             W.sptr[lane] = p;
-            W.lval[lane] = lv ? 1 : 0;
-            W.vcn[lane] = vc;
         }
         wave_sync_lds();
         if (lane == 0) {
-            uint32_t acc = 0, vacc = 0;
+            uint32_t acc = 0;
             bool dn = (fp.diag & 2) != 0;
 #pragma unroll 1
             for (int j = 0; j < kWinSlots; ++j) {
                 W.pre[j] = acc;
                 const uint32_t c = W.scnt[j];
                 if (c > cap) dn = true; else acc += c;
-                const uint32_t vn = min(W.vcn[j], kVirt - vacc);
-                W.vbs[j] = vacc;
-                W.vcn[j] = vn;
-                vacc += vn;
             }
             if (acc > kWinRecs) dn = true;
             W.pre[kWinSlots] = dn ? 0 : acc;
             W.nrec = dn ? 0 : acc;
-            W.nv0 = dn ? 0 : vacc;
             W.nvirt = dn ? 1u : 0u;  // (the dense flag, for the other lanes)
         }
         wave_sync_lds();
@@ -2039,66 +1760,27 @@ __global__ __launch_bounds__(kResThreads, CDC_RES_MINW) void resolve_kernel(cons
             if (L.act && !L.first && (fp.diag & 1)) s0 = L.off;  // test hook: no warm-up
             walk_lanes(st, fp, cand, tab, W, ch, L, lane, L.act, s0, cnt, entry, exit, steps);
         } else {
+            const uint32_t nrec = W.nrec;
             {
-                // records, and their links from the scan where it made them
-                uint32_t v[kWinSlots], ld[kWinSlots];
-                uint16_t lt[kWinSlots];
+                uint32_t v[kWinSlots];
 #pragma unroll
                 for (int j = 0; j < kWinSlots; ++j) {
                     const uint32_t c = W.scnt[j];
-                    const uint64_t i = lane < c ? (uint64_t)(gfirst + j) * cap + lane : 0;
-                    v[j] = cand.pos[i];
-                    const uint64_t il = lane < c && W.lval[j] ? i : 0;
-                    ld[j] = lk.ldist[il];
-                    lt[j] = lk.ltgt[il];
+                    v[j] = cand.pos[lane < c ? (uint64_t)(gfirst + j) * cap + lane : 0];
                 }
 #pragma unroll 1
                 for (int j = 0; j < kWinSlots; ++j) {
                     const uint64_t kb = skey(W.ssi[j]) | W.soff[j];
                     const uint32_t c = W.scnt[j], p0 = W.pre[j];
-                    const bool lv = W.lval[j] != 0;
                     for (uint32_t k = lane; k < c; k += 64) {  // (k >= 64: rare dense-ish slots)
-                        const uint64_t i = (uint64_t)(gfirst + j) * cap + k;
-                        const uint32_t r = k < 64 ? v[0] : cand.pos[i];
+                        const uint32_t r = k < 64 ? v[0] : cand.pos[(uint64_t)(gfirst + j) * cap + k];
                         W.rec[p0 + k] = r;
                         W.key[p0 + k] = kb + (r & kCandPosMask);
                         W.rslot[p0 + k] = (uint8_t)j;
-                        const uint32_t d = !lv ? 0u : k < 64 ? ld[0] : lk.ldist[i];
-                        const uint32_t t = !lv ? kTgtNone : k < 64 ? lt[0] : lk.ltgt[i];
-                        W.link[p0 + k] = d;
-                        W.lrec[p0 + k] = d ? tgt_entry(W, t, j) : (uint16_t)0;
                     }
 #pragma unroll
-                    for (int q = 0; q + 1 < kWinSlots; ++q) {  // next slot's batch into [0]
-                        v[q] = v[q + 1];
-                        ld[q] = ld[q + 1];
-                        lt[q] = lt[q + 1];
-                    }
+                    for (int q = 0; q + 1 < kWinSlots; ++q) v[q] = v[q + 1];  // next slot's batch into v[0]
                 }
-                // the scan's virtual entries of every slot (<= kVirtSpan each)
-                constexpr int kVI = (kWinSlots * kVirtSpan + 63) / 64;
-                uint4 ve[kVI];
-#pragma unroll
-                for (int i = 0; i < kVI; ++i) {
-                    const uint32_t x = lane + 64 * i;
-                    const int j = (int)(x / kVirtSpan);
-                    const bool in = x < kWinSlots * kVirtSpan && x % kVirtSpan < W.vcn[j < kWinSlots ? j : 0];
-                    ve[i] = lk.vent[in ? (uint64_t)(gfirst + j) * kVirtSpan + x % kVirtSpan : 0];
-                }
-#pragma unroll
-                for (int i = 0; i < kVI; ++i) {
-                    const uint32_t x = lane + 64 * i;
-                    const int j = (int)(x / kVirtSpan);
-                    const uint32_t vv = x % kVirtSpan;
-                    if (x < kWinSlots * kVirtSpan && vv < W.vcn[j]) {
-                        const uint32_t e = W.vbs[j] + vv;
-                        W.vpos[e] = W.soff[j] + ve[i].x;
-                        W.vslot[e] = (uint8_t)j;
-                        W.link[kWinRecs + e] = ve[i].y;
-                        W.lrec[kWinRecs + e] = ve[i].y ? tgt_entry(W, ve[i].z, j) : (uint16_t)0;
-                    }
-                }
-                for (uint32_t e = W.nv0 + lane; e < kVirt; e += 64) W.link[kWinRecs + e] = 0;  // new ones: unknown
             }
             wave_sync_lds();
             CDC_DIAG_T(1);
@@ -2107,10 +1789,9 @@ __global__ __launch_bounds__(kResThreads, CDC_RES_MINW) void resolve_kernel(cons
             // chunk start after a chunk starting there -- by an LDS search.
             // Next starts that are neither records nor past the walked slots
             // become new virtual entries.
-            // (records of the searched-only slot keep the scan's links, or 0:
-            // they are never walked from)
             const uint32_t nlink = W.pre[kReach];
-            uint32_t nv = W.nv0, e0 = 0, e1 = nlink;
+            for (uint32_t i = nlink + lane; i < nrec; i += 64) W.link[i] = 0;  // searched only
+            uint32_t nv = 0, e0 = 0, e1 = nlink;
             bool virt = false;
             for (;;) {
                 // (the next pass's bytes are loaded while this pass evaluates:
@@ -2303,14 +1984,14 @@ __global__ __launch_bounds__(kResThreads, CDC_RES_MINW) void resolve_kernel(cons
 }  // namespace
 
 hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
-                       const Candidates &cand, const Links &lk, const Compact &cp, const uint64_t *d_tails,
-                       uint32_t n_tails, int num_cus, hipStream_t s) {
+                       const Candidates &cand, const Compact &cp, const uint64_t *d_tails, uint32_t n_tails,
+                       int num_cus, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
     if (n_tails) {
         if (fp.cm_align)
-            scan_tail_kernel<true><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, lk, d_tails);
+            scan_tail_kernel<true><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, d_tails);
         else
-            scan_tail_kernel<false><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, lk, d_tails);
+            scan_tail_kernel<false><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, d_tails);
     }
     // 16 waves per CU (the 128-VGPR budget), GEAR lookups one dword ahead of
     // the chain.  (Measured: 12 waves with two dwords of lookahead is slower.)
@@ -2328,24 +2009,24 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
     const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
     if (mode == 1 && fp.cm_align)
-        scan_kernel<true, W, K, 1><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, lk, cp);
+        scan_kernel<true, W, K, 1><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else if (mode == 2 && fp.cm_align)
-        scan_kernel<true, W, K, 2><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, lk, cp);
+        scan_kernel<true, W, K, 2><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else if (fp.cm_align)
-        scan_kernel<true, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, lk, cp);
+        scan_kernel<true, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else
-        scan_kernel<false, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, lk, cp);
+        scan_kernel<false, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     return hipGetLastError();
 }
 
 uint64_t resolve_blocks(uint64_t spans) { return (spans + kBlockSpans - 1) / kBlockSpans; }
 
 hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
-                          const Candidates &cand, const Links &lk, const Chains &ch, const Compact &cp,
-                          const Resolve &rs, void *d_out, uint64_t out_cap, hipStream_t s) {
+                          const Candidates &cand, const Chains &ch, const Compact &cp, const Resolve &rs,
+                          void *d_out, uint64_t out_cap, hipStream_t s) {
     if (!st.total_spans) return hipSuccess;
     resolve_kernel<<<(unsigned)resolve_blocks(st.total_spans), kResThreads, 0, s>>>(
-        st, fp, d_gear, cand, lk, ch, cp, rs, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap);
+        st, fp, d_gear, cand, ch, cp, rs, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap);
     return hipGetLastError();
 }
 

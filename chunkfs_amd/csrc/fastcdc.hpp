@@ -37,29 +37,6 @@ struct Resolve {
     uint64_t gen;
 };
 
-// Record links computed by the scan kernel between spans (fastcdc.hip
-// "links in the scan"): for every candidate record of a span, the next chunk
-// start after a chunk starting there, and a small table of the span's
-// "virtual" entries (next starts that are not records: max cuts, hits in the
-// truncated region) with their own links.  The resolve loads them instead of
-// computing them; a span whose lvalid word is not this batch's generation, or
-// a link of 0, is computed by the resolve as before.
-constexpr uint32_t kVirtSpan = 16;          // virtual entries per span
-constexpr uint16_t kTgtEnd = 0xFFFF;        // next start = the stream end
-constexpr uint16_t kTgtNone = 0xFFFE;       // next start known, not an entry
-constexpr uint16_t kTgtVirt = 0x8000;       // | v: virtual entry v of the same span
-constexpr uint32_t kTgtDeltaShift = 12;     // record target: delta (0 / 1 span on) << 12 | index
-
-struct Links {
-    uint32_t *ldist;   // [spans*cap]: next start - record position (0: unknown)
-    uint16_t *ltgt;    // [spans*cap]: kTgt* or delta << 12 | record index
-    uint32_t *vcnt;    // [spans]: virtual entries
-    uint4 *vent;       // [spans*kVirtSpan]: {position - span start, dist (0: unknown), target, 0}
-    uint32_t *done;    // [spans]: gen once the span's records are stored (write-through)
-    uint32_t *lvalid;  // [spans]: gen once the span's links are stored
-    uint32_t gen;      // batch generation (never 0)
-};
-
 // stats words (reset by the scan kernel of the batch)
 constexpr int kStatCand = 0;      // candidate records
 constexpr int kStatOvf = 1;       // spans whose record list overflowed
@@ -77,11 +54,11 @@ uint64_t resolve_blocks(uint64_t spans);
 
 // d_tails[n_tails]: span ids of the ragged last spans (scanned by their own kernel).
 hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
-                       const Candidates &cand, const Links &lk, const Compact &cp, const uint64_t *d_tails,
-                       uint32_t n_tails, int num_cus, hipStream_t s);
+                       const Candidates &cand, const Compact &cp, const uint64_t *d_tails, uint32_t n_tails,
+                       int num_cus, hipStream_t s);
 hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
-                          const Candidates &cand, const Links &lk, const Chains &ch, const Compact &cp,
-                          const Resolve &rs, void *d_out, uint64_t out_cap, hipStream_t s);
+                          const Candidates &cand, const Chains &ch, const Compact &cp, const Resolve &rs,
+                          void *d_out, uint64_t out_cap, hipStream_t s);
 
 }  // namespace p3
 }  // namespace cdc
