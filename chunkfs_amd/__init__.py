@@ -105,6 +105,7 @@ class Chunker:
             raise NotImplementedError(L.cdc_last_error().decode())
         check(rc)
         self._h = h
+        self._pending = []  # first[] arrays of enqueued batches (chunk_batch_device_async)
         self.device = device
 
     def close(self):
@@ -186,6 +187,27 @@ class Chunker:
                                            out_cap, ctypes.c_void_p(first.ctypes.data),
                                            ctypes.c_void_p(int(stream))))
         return first
+
+    def chunk_batch_device_async(self, d_ptrs, lens, d_out_ptr, out_cap, stream=0):
+        """cdc_chunk_batch_device_async: enqueue the batch (FastCDC batches of
+        more than 8 MiB are pipelined: the next batch's scan launch resolves
+        it).  Returns its first[n+1] array, filled by batch_sync()."""
+        ptrs = np.ascontiguousarray(np.asarray(d_ptrs, dtype=np.uint64))
+        lens_a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+        n = int(lens_a.size)
+        first = np.zeros(n + 1, dtype=np.uint64)
+        self.__dict__.setdefault("_pending", []).append(first)  # the library writes it at batch_sync()
+        check(lib().cdc_chunk_batch_device_async(self._h, n, ctypes.c_void_p(ptrs.ctypes.data),
+                                                 ctypes.c_void_p(lens_a.ctypes.data),
+                                                 ctypes.c_void_p(int(d_out_ptr)), out_cap,
+                                                 ctypes.c_void_p(first.ctypes.data), ctypes.c_void_p(int(stream))))
+        return first
+
+    def batch_sync(self):
+        """cdc_batch_sync: complete every enqueued batch; the last one's chunk count."""
+        r = check(lib().cdc_batch_sync(self._h))
+        self._pending = []
+        return r
 
     def batch_max_chunks(self, lens):
         n = len(lens)

@@ -22,7 +22,8 @@ ALGO = {"fast": 0, "fixed": 1, "rabin": 2, "super": 3, "ultra": 4, "leap": 5, "s
 EXPORTS = [
     "cdc_create", "cdc_create_seq", "cdc_destroy", "cdc_chunk_data", "cdc_estimate_chunk_count",
     "cdc_max_chunk_count", "cdc_describe", "cdc_last_error", "cdc_set_gear", "cdc_set_rabin_poly",
-    "cdc_chunk_batch_device", "cdc_batch_max_chunks", "cdc_last_timing",
+    "cdc_chunk_batch_device", "cdc_chunk_batch_device_async", "cdc_batch_sync", "cdc_batch_max_chunks",
+    "cdc_last_timing",
     "cdc_fs_write", "cdc_write_begin", "cdc_write_segment", "cdc_write_drain", "cdc_write_finish",
     "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
     "cdc_index_create", "cdc_index_destroy", "cdc_index_clear", "cdc_index_insert_device",
@@ -31,6 +32,7 @@ EXPORTS = [
 ]
 # include/chunkfs_amd_debug.h (diagnostics, not part of the drop-in boundary)
 DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy", "cdc_debug_host_stats",
+                 "cdc_debug_read_bw",
                  "cdc_debug_timing_back"]
 
 
@@ -116,6 +118,10 @@ def lib():
     L.cdc_set_rabin_poly.restype = ctypes.c_int
     L.cdc_chunk_batch_device.argtypes = [P, sz, P, P, P, sz, P, P]
     L.cdc_chunk_batch_device.restype = ctypes.c_int64
+    L.cdc_chunk_batch_device_async.argtypes = [P, sz, P, P, P, sz, P, P]
+    L.cdc_chunk_batch_device_async.restype = ctypes.c_int64
+    L.cdc_batch_sync.argtypes = [P]
+    L.cdc_batch_sync.restype = ctypes.c_int64
     L.cdc_batch_max_chunks.argtypes = [P, sz, u64p]
     L.cdc_batch_max_chunks.restype = sz
     L.cdc_last_timing.argtypes = [P, ctypes.POINTER(cdc_timing_t), sz]
@@ -154,6 +160,8 @@ def lib():
     L.cdc_debug_pipeline.restype = ctypes.c_int
     L.cdc_debug_record_cap.argtypes = [P]
     L.cdc_debug_record_cap.restype = ctypes.c_uint32
+    L.cdc_debug_read_bw.argtypes = [P, P, sz, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    L.cdc_debug_read_bw.restype = ctypes.c_int
     L.cdc_debug_copy.argtypes = [P, ctypes.c_int, P, sz]
     L.cdc_debug_copy.restype = ctypes.c_int64
     L.cdc_version.argtypes = []

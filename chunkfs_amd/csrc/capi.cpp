@@ -85,6 +85,19 @@ int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
                                          static_cast<hipStream_t>(hip_stream));
 }
 
+int64_t cdc_chunk_batch_device_async(cdc_handle_t *h, size_t n, const uint8_t *const *d_streams,
+                                     const uint64_t *lens, cdc_chunk_t *d_out, size_t out_cap, uint64_t *first,
+                                     void *hip_stream) {
+    if (!h) return bad_handle();
+    return h->engine->chunk_batch_device_async(n, d_streams, lens, d_out, out_cap, first,
+                                               static_cast<hipStream_t>(hip_stream));
+}
+
+int64_t cdc_batch_sync(cdc_handle_t *h) {
+    if (!h) return bad_handle();
+    return h->engine->batch_sync();
+}
+
 size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n, const uint64_t *lens) {
     return (h && lens) ? h->engine->batch_max_chunks(n, lens) : 0;
 }
@@ -96,6 +109,11 @@ int cdc_debug_timing_back(cdc_handle_t *h, uint32_t back, cdc_timing_t *t, size_
     if (rc) return rc;
     std::memcpy(t, &v, t_size < sizeof v ? t_size : sizeof v);
     return CDC_OK;
+}
+
+int cdc_debug_read_bw(cdc_handle_t *h, const uint8_t *d_buf, size_t len, int reps, double *ms) {
+    if (!h || !ms || (len && !d_buf) || reps < 1) return (int)bad_handle();
+    return h->engine->read_bw(d_buf, len, reps, ms);
 }
 
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size) {

@@ -58,5 +58,8 @@ struct Candidates {
 hipError_t launch_fixed(const StreamTable &st, uint64_t chunk_size, const uint64_t *d_first, void *d_out,
                         uint64_t total, hipStream_t s);
 hipError_t launch_fill_splitmix64(uint8_t *d_buf, uint64_t len, uint64_t seed, hipStream_t s);
+// Read-only XOR reduction of len bytes (16-byte multiple used): one word per
+// block into d_out[num_cus * 8] (zeroed by the caller).
+hipError_t launch_read_reduce(const uint8_t *d_buf, uint64_t len, uint64_t *d_out, int num_cus, hipStream_t s);
 
 }  // namespace cdc

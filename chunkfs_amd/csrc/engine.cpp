@@ -189,6 +189,7 @@ int Engine::init() {
 
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
+    if (fb_any_) (void)fast_drain();
     if (own_stream_) (void)hipStreamSynchronize(own_stream_);
     (void)hipFree(ws_);
     (void)hipFree(small_mem_);
@@ -223,6 +224,10 @@ int Engine::set_gear(const uint64_t *gear) {
         set_error("gear is NULL");
         return CDC_EINVAL;
     }
+    if (fb_any_) {  // the batches in flight finish with the table they were submitted with
+        const int64_t r = fast_drain();
+        if (r < 0) return (int)r;
+    }
     if (wr_.active) {  // windows already chunked used the old table: a write never mixes two
         set_error("cdc_set_gear: a streaming write is in progress (cdc_write_finish it first)");
         return CDC_EINVAL;
@@ -246,15 +251,24 @@ size_t Engine::batch_max_chunks(size_t n, const uint64_t *lens) const {
 
 int Engine::ensure_host_staging(size_t n) {
     if (h_stage_ && h_stage_streams_ >= n) return CDC_OK;
+    if (fb_any_) {  // (the batches in flight read their slots)
+        set_error("internal: host staging regrown with FastCDC batches in flight");
+        return CDC_EINVAL;
+    }
     (void)hipHostFree(h_stage_);
     h_stage_ = nullptr;
     const size_t want = n + 64;
-    // ptrs[W] lens[W] span_base[W] tails[W] | stats ++ first[n+1] (fixed: first[n+1])
-    // stream tables 4 n, device-written stats / flags ++ first[n+1] (n + 32),
-    // the walk's flags[4] and fix-up round flag blocks (4 x walk::kMaxFixRounds)
-    HIP_TRY(hipHostMalloc(&h_stage_, (5 * want + 36 + 4 * walk::kMaxFixRounds) * sizeof(uint64_t),
-                          hipHostMallocCoherent));
+    // Per slot: ptrs[W] lens[W] span_base[W] tails[W] | stats ++ first[n+1]
+    // (fixed: first[n+1]) -- stream tables 4 n, device-written stats / flags
+    // ++ first[n+1] (n + 32), the walk's flags[4] and fix-up round flag blocks
+    // (4 x walk::kMaxFixRounds).  Slot 1: the second FastCDC batch in flight.
+    const size_t per = 5 * want + 36 + 4 * walk::kMaxFixRounds;
+    HIP_TRY(hipHostMalloc(&h_stage_, kSlots * per * sizeof(uint64_t), hipHostMallocCoherent));
     h_stage_streams_ = want;
+    for (int k = 0; k < kSlots; ++k) {
+        fs_[k].h = static_cast<uint64_t *>(h_stage_) + k * per;
+        fs_[k].tables.clear();
+    }
     return CDC_OK;
 }
 
@@ -271,13 +285,26 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
         off = align_up(off + bytes, A);
         return o;
     };
-    const size_t o_count = take(S * 4), o_pos = take(S * cap * 4);
+    if (fb_any_) {
+        set_error("internal: workspace regrown with FastCDC batches in flight");
+        return CDC_EINVAL;
+    }
+    size_t o_count[kSlots], o_pos[kSlots], o_ptrs[kSlots], o_lens[kSlots], o_sb[kSlots], o_stats[kSlots],
+        o_tails[kSlots];
+    for (int k = 0; k < kSlots; ++k) {  // per batch in flight (FastCDC); the fixed-size path uses slot 0
+        o_count[k] = take(S * 4);
+        o_pos[k] = take(S * cap * 4);
+        o_ptrs[k] = take(N * 8);
+        o_lens[k] = take(N * 8);
+        o_sb[k] = take((N + 1) * 8);
+        o_stats[k] = take(p3::kStatWords * 8);
+        o_tails[k] = take(N * 8);
+    }
     const size_t o_starts = take(S * smax * 8);  // chunk starts beyond the LDS-resident ones
     const size_t o_first = take((N + 1) * 8);
-    const size_t o_ptrs = take(N * 8), o_lens = take(N * 8), o_sb = take((N + 1) * 8);
-    const uint64_t nb = p3::resolve_blocks(S) + 2;
-    const size_t o_stats = take(p3::kStatWords * 8), o_desc = take(6 * nb * 8);
-    const size_t o_tails = take(N * 8);
+    const uint64_t nb = p3::resolve_units(S) + 2;
+    const size_t o_desc = take(6 * nb * 8);
+    const size_t o_part = take((size_t)p3::resolve_part_words(num_cus_) * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
     ws_spans_ = 0;
@@ -288,20 +315,30 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     ws_spans_ = S;
     ws_streams_ = N;
     char *b = static_cast<char *>(ws_);
-    cand_.cap = (uint32_t)cap;
-    cand_.count = reinterpret_cast<uint32_t *>(b + o_count);
-    cand_.pos = reinterpret_cast<uint32_t *>(b + o_pos);
+    for (int k = 0; k < kSlots; ++k) {
+        FastSlot &f = fs_[k];
+        f.cand.cap = (uint32_t)cap;
+        f.cand.count = reinterpret_cast<uint32_t *>(b + o_count[k]);
+        f.cand.pos = reinterpret_cast<uint32_t *>(b + o_pos[k]);
+        f.d_ptrs = reinterpret_cast<const uint8_t **>(b + o_ptrs[k]);
+        f.d_lens = reinterpret_cast<uint64_t *>(b + o_lens[k]);
+        f.d_sb = reinterpret_cast<uint64_t *>(b + o_sb[k]);
+        f.d_tails = reinterpret_cast<uint64_t *>(b + o_tails[k]);
+        f.stats = reinterpret_cast<uint64_t *>(b + o_stats[k]);
+        f.tables.clear();
+    }
+    cand_ = fs_[0].cand;
     d_first_ = reinterpret_cast<uint64_t *>(b + o_first);
-    d_ptrs_ = reinterpret_cast<const uint8_t **>(b + o_ptrs);
-    d_lens_ = reinterpret_cast<uint64_t *>(b + o_lens);
-    d_span_base_ = reinterpret_cast<uint64_t *>(b + o_sb);
+    d_ptrs_ = fs_[0].d_ptrs;  // (the fixed-size path)
+    d_lens_ = fs_[0].d_lens;
+    d_span_base_ = fs_[0].d_sb;
     ch3_.smax = (uint32_t)smax;
     ch3_.starts = reinterpret_cast<uint64_t *>(b + o_starts);
-    cp3_.stats = reinterpret_cast<uint64_t *>(b + o_stats);
     uint64_t *desc = reinterpret_cast<uint64_t *>(b + o_desc);
     rs3_ = p3::Resolve{desc, desc + nb, desc + 2 * nb, desc + 3 * nb, desc + 4 * nb, desc + 5 * nb, 0};
     HIP_TRY(hipMemset(desc, 0, 6 * nb * 8));  // no stale status word can carry a live generation
-    d_tails_ = reinterpret_cast<uint64_t *>(b + o_tails);
+    d_tails_ = fs_[0].d_tails;
+    d_part_ = reinterpret_cast<uint64_t *>(b + o_part);
     return CDC_OK;
 }
 
@@ -309,6 +346,22 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
                                    const uint64_t *lens, cdc_chunk_t *d_out,
                                    size_t out_cap, uint64_t *first,
                                    hipStream_t stream) {
+    return batch_device(n, d_streams, lens, d_out, out_cap, first, stream, false);
+}
+
+int64_t Engine::chunk_batch_device_async(size_t n, const uint8_t *const *d_streams, const uint64_t *lens,
+                                         cdc_chunk_t *d_out, size_t out_cap, uint64_t *first,
+                                         hipStream_t stream) {
+    return batch_device(n, d_streams, lens, d_out, out_cap, first, stream, true);
+}
+
+int64_t Engine::batch_sync() {
+    HIP_TRY(hipSetDevice(device_));
+    return fast_drain();
+}
+
+int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
+                             size_t out_cap, uint64_t *first, hipStream_t stream, bool async) {
     if (n && (!d_streams || !lens || !first)) {
         set_error("cdc_chunk_batch_device: NULL argument");
         return CDC_EINVAL;
@@ -319,10 +372,6 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     }
     HIP_TRY(hipSetDevice(device_));
     hipStream_t s = stream ? stream : own_stream_;
-    const double hash_ms = timing_.hash_ms;  // (reported with the batch it hashed)
-    timing_pending_ = false;                 // (a new batch re-records the events)
-    timing_ = cdc_timing_t{};
-    timing_.hash_ms = hash_ms;
     uint64_t bytes = 0, need = 0;
     for (size_t i = 0; i < n; ++i) {
         bytes += lens[i];
@@ -338,12 +387,28 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
             return CDC_EINVAL;
         }
     }
-    timing_.bytes = bytes;
-    out_cap_ = out_cap;
     if (need > out_cap) {
         set_error("out_cap < cdc_batch_max_chunks()");
         return CDC_EINVAL;
     }
+    // FastCDC multi-megabyte batches are pipelined; everything else runs to
+    // completion here, after the batches in flight.
+    const bool pipe = algo_ == CDC_ALGO_FASTCDC && n > 0 && bytes > kSmallBatch;
+    if (!pipe && fb_any_) {
+        const int64_t r = fast_drain();
+        if (r < 0) return r;
+    }
+    if (pipe) {
+        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s);
+        if (r < 0 || async) return r;
+        return fast_drain();
+    }
+    const double hash_ms = timing_.hash_ms;  // (reported with the batch it hashed)
+    timing_pending_ = false;                 // (a new batch re-records the events)
+    timing_ = cdc_timing_t{};
+    timing_.hash_ms = hash_ms;
+    timing_.bytes = bytes;
+    out_cap_ = out_cap;
     if (n == 0) {
         if (first) first[0] = 0;
         return 0;
@@ -356,28 +421,20 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
         if (rc < 0) return rc;
         // (kSmallFallback: the regular pipeline below)
     }
+    if (algo_ == CDC_ALGO_FASTCDC) {  // small batches: one scan + resolve, waited for here
+        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s);
+        if (r < 0) return r;
+        return fast_drain();
+    }
     uint64_t *h = static_cast<uint64_t *>(h_stage_);
     uint64_t *h_ptrs = h, *h_lens = h + h_stage_streams_, *h_sb = h + 2 * h_stage_streams_;
-    uint64_t *h_tails = h + 3 * h_stage_streams_;
-    // Small FastCDC batches (the host path's 1 MiB chunk_data calls) use the
-    // shortest spans the kernels allow (>= max, >= 16 KiB: 256 B per scan
-    // lane): 4x the lanes and a 4x shorter serial scan per lane, for latency.
-    const uint32_t sl2 = algo_ == CDC_ALGO_FASTCDC ? (bytes <= kSmallBatch ? small_span_log2_ : span_log2_)
-                         : is_walk()               ? seg_log2_
-                                                   : 0;
+    const uint32_t sl2 = is_walk() ? seg_log2_ : 0;
     uint64_t spans = 0;
-    uint32_t n_tails = 0;
     for (size_t i = 0; i < n; ++i) {
         h_ptrs[i] = reinterpret_cast<uint64_t>(d_streams[i]);
         h_lens[i] = lens[i];
         h_sb[i] = spans;
-        if (algo_ == CDC_ALGO_FASTCDC) {
-            const uint64_t k = (lens[i] + (1ull << sl2) - 1) >> sl2;
-            spans += k;
-            if (lens[i] & ((1ull << sl2) - 1)) h_tails[n_tails++] = spans - 1;  // ragged last span
-        } else if (is_walk()) {
-            spans += (lens[i] + (1ull << sl2) - 1) >> sl2;  // segments
-        }
+        if (is_walk()) spans += (lens[i] + (1ull << sl2) - 1) >> sl2;  // segments
     }
     h_sb[n] = spans;
     if (algo_ != CDC_ALGO_FIXED && spans == 0) {  // every stream is empty
@@ -395,12 +452,10 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     const bool same = zero_copy || (ws_gen_ == tables_gen_ && tables_.size() == 2 * n &&
                                     std::memcmp(tables_.data(), h_ptrs, n * 8) == 0 &&
                                     std::memcmp(tables_.data() + n, h_lens, n * 8) == 0);
-    cur_tails_ = zero_copy ? h_tails : d_tails_;
     if (!same) {
         HIP_TRY(hipMemcpyAsync(d_ptrs_, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_lens_, h_lens, n * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(d_span_base_, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
-        if (n_tails) HIP_TRY(hipMemcpyAsync(d_tails_, h_tails, n_tails * 8, hipMemcpyHostToDevice, s));
         tables_.assign(h_ptrs, h_ptrs + n);
         tables_.insert(tables_.end(), h_lens, h_lens + n);
         tables_gen_ = ws_gen_;
@@ -412,77 +467,206 @@ int64_t Engine::chunk_batch_device(size_t n, const uint8_t *const *d_streams,
     st.n = (uint32_t)n;
     st.span_log2 = sl2;
     st.total_spans = spans;
-    last_spans_ = algo_ == CDC_ALGO_FASTCDC ? spans : 0;
-    n_tails_ = n_tails;
-    rc = algo_ == CDC_ALGO_FASTCDC ? run_fast(st, d_out, n, first, s)
-         : is_walk()               ? run_walk(st, d_out, n, first, s)
-                                   : run_fixed(st, n, lens, d_out, first, s);
+    rc = is_walk() ? run_walk(st, d_out, n, first, s) : run_fixed(st, n, lens, d_out, first, s);
     if (rc) return rc;
     return (int64_t)first[n];
 }
 
-int Engine::run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
-                        uint64_t *first, hipStream_t s) {
-    uint64_t *h = static_cast<uint64_t *>(h_stage_);
-    uint64_t *h_misc = h + 4 * h_stage_streams_;  // stats ++ first[n+1], written by the device
-    p3::Compact cp = cp3_;
-    cp.h_stats = h_misc;
-    cp.h_first = h_misc + p3::kStatWords;
-    h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the last resolve block
+// One FastCDC batch into the pipeline: its tables into the batch's slot, then
+// ONE launch that scans it and resolves the pending previous batch (if any).
+// The batch itself is resolved by the next submit's launch or by fast_drain().
+int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
+                            size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s) {
+    if (fb_any_ && s != fb_stream_) {  // one pipeline per stream
+        const int64_t r = fast_drain();
+        if (r < 0) return r;
+    }
+    const uint32_t sl2 = bytes <= kSmallBatch ? small_span_log2_ : span_log2_;
+    uint64_t spans = 0;
+    for (size_t i = 0; i < n; ++i) spans += (lens[i] + (1ull << sl2) - 1) >> sl2;
+    const bool zero_copy = bytes <= kSmallBatch && n <= kZeroCopyStreams;
+    const bool grow = !(h_stage_ && h_stage_streams_ >= n) || !(ws_ && spans <= ws_spans_ && n <= ws_streams_);
+    if (fb_any_ && (zero_copy || grow)) {  // (buffers the batches in flight use)
+        const int64_t r = fast_drain();
+        if (r < 0) return r;
+    }
+    const uint64_t seq = fb_seq_;
+    if (fb_[seq % 3].live) {  // batch seq-3: the stats block this launch's resolve writes next
+        const int rc = fast_collect((int)(seq % 3));
+        if (rc) {
+            (void)fast_drain();
+            return rc;
+        }
+    }
+    int rc = ensure_host_staging(n);
+    if (rc) return rc;
+    rc = ensure_workspace(spans ? spans : 1, n);
+    if (rc) return rc;
+    const int slot = (int)(seq % kSlots);
+    FastSlot &f = fs_[slot];
+    uint64_t *h_ptrs = f.h, *h_lens = f.h + h_stage_streams_, *h_sb = f.h + 2 * h_stage_streams_;
+    uint64_t *h_tails = f.h + 3 * h_stage_streams_;
+    bool same = !zero_copy && f.tables_gen == ws_gen_ && f.tables.size() == 2 * n;
+    for (size_t i = 0; same && i < n; ++i)
+        same = f.tables[i] == reinterpret_cast<uint64_t>(d_streams[i]) && f.tables[n + i] == lens[i];
+    if (!same) {
+        // (the slot's previous H2D copies ran before the launch two batches
+        // back, which was collected or is ahead of this one on the stream)
+        uint64_t sp = 0;
+        uint32_t nt = 0;
+        for (size_t i = 0; i < n; ++i) {
+            h_ptrs[i] = reinterpret_cast<uint64_t>(d_streams[i]);
+            h_lens[i] = lens[i];
+            h_sb[i] = sp;
+            sp += (lens[i] + (1ull << sl2) - 1) >> sl2;
+            if (lens[i] & ((1ull << sl2) - 1)) h_tails[nt++] = sp - 1;  // ragged last span
+        }
+        h_sb[n] = sp;
+        f.n_tails = nt;
+        f.tables.clear();
+        if (!zero_copy) {
+            HIP_TRY(hipMemcpyAsync(f.d_ptrs, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(f.d_lens, h_lens, n * 8, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemcpyAsync(f.d_sb, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
+            if (nt) HIP_TRY(hipMemcpyAsync(f.d_tails, h_tails, nt * 8, hipMemcpyHostToDevice, s));
+            f.tables.assign(h_ptrs, h_ptrs + n);
+            f.tables.insert(f.tables.end(), h_lens, h_lens + n);
+            f.tables_gen = ws_gen_;
+        }
+    }
+    StreamTable st{};
+    st.ptrs = zero_copy ? reinterpret_cast<const uint8_t *const *>(h_ptrs) : f.d_ptrs;
+    st.lens = zero_copy ? h_lens : f.d_lens;
+    st.span_base = zero_copy ? h_sb : f.d_sb;
+    st.n = (uint32_t)n;
+    st.span_log2 = sl2;
+    st.total_spans = spans;
+    uint64_t *h_misc = f.h + 4 * h_stage_streams_;  // stats ++ first[n+1], written by the device
+    const p3::Compact cp{f.stats, h_misc, h_misc + p3::kStatWords};
+    h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the resolve's last block
+    if (!spans) {  // every stream is empty: nothing to launch
+        h_misc[p3::kStatDone] = 1;
+        h_misc[p3::kStatError] = 0;
+        for (size_t i = 0; i <= n; ++i) cp.h_first[i] = 0;
+    }
     p3::Resolve rs = rs3_;
     rs.gen = ++res_gen_;
-    hipEvent_t *ev = tev_[fast_batches_ % kTimeRing];
+    FastBatch *prev = nullptr;
+    if (fb_any_) {
+        FastBatch &pb = fb_[(seq + 2) % 3];  // batch seq-1
+        if (pb.live && !pb.resolved) prev = &pb;
+    }
+    FastBatch &rec = fb_[seq % 3];
+    rec = FastBatch{};
+    rec.live = true;
+    rec.resolved = spans == 0;
+    rec.slot = slot;
+    rec.n = n;
+    rec.first = first;
+    rec.seq = seq;
+    rec.bytes = bytes;
+    rec.ra = p3::ResArgs{st, f.cand, ch3_, cp, rs, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap,
+                         p3::resolve_units(spans), d_part_};
+    hipEvent_t *ev = tev_[seq % kTimeRing];
     HIP_TRY(hipEventRecord(ev[0], s));
-    HIP_TRY(p3::launch_scan(st, fp_, d_gear_, cand_, cp, cur_tails_, n_tails_, num_cus_, s));
+    if (spans || prev) {
+        const p3::ResArgs none{};
+        HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails,
+                                num_cus_, prev ? prev->ra : none, s));
+    }
     HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, cand_, ch3_, cp, rs, d_out, out_cap_, s));
-    HIP_TRY(hipEventRecord(ev[2], s));
-    ++fast_batches_;
-    // The resolve's last block writes the done word into coherent pinned
-    // memory after a system-scope fence: spin on it (wakes faster than a
-    // blocking stream sync) for about the batch's expected device time
-    // (bytes at ~2 TB/s, 0.1-2 ms), pausing between polls, then the stream
-    // sync confirms (at most 2 ms of spinning).  Long batches or a busy
-    // caller stream fall through to the blocking sync instead of burning a core.
+    if (prev) {
+        prev->resolved = true;
+        HIP_TRY(hipEventRecord(tev_[prev->seq % kTimeRing][2], s));
+    }
+    if (rec.resolved) HIP_TRY(hipEventRecord(ev[2], s));
+    fb_seq_ = seq + 1;
+    fast_batches_ = fb_seq_;
+    fb_any_ = true;
+    fb_stream_ = s;
+    cand_ = f.cand;
+    last_spans_ = spans;
+    return 0;
+}
+
+// The last batch's resolve on its own, then every batch in flight collected
+// in order.  Returns the last batch's chunk count.
+int64_t Engine::fast_drain() {
+    if (!fb_any_) return 0;
+    const uint64_t last = fb_seq_ - 1;
+    FastBatch &lb = fb_[last % 3];
+    int rc = CDC_OK;
+    if (lb.live && !lb.resolved) {
+        lb.resolved = true;
+        const hipError_t e = p3::launch_resolve(lb.ra, fp_, d_gear_, num_cus_, fb_stream_);
+        if (e != hipSuccess) {
+            set_error(std::string("launch_resolve: ") + hipGetErrorString(e));
+            rc = CDC_EDEVICE;
+        }
+        (void)hipEventRecord(tev_[lb.seq % kTimeRing][2], fb_stream_);
+    }
+    int64_t total = 0;
+    for (uint64_t q = last >= 2 ? last - 2 : 0; q <= last; ++q) {
+        FastBatch &b = fb_[q % 3];
+        if (!b.live || b.seq != q) continue;
+        const int r = rc ? rc : fast_collect((int)(q % 3));
+        b.live = false;
+        if (r && !rc) rc = r;
+        if (q == last && !rc) total = (int64_t)b.first[b.n];
+    }
+    if (rc) (void)hipStreamSynchronize(fb_stream_);  // (nothing of a failed pipeline stays in flight)
+    fb_any_ = false;
+    return rc ? rc : total;
+}
+
+// Wait for batch record k's resolve (its last block writes the done word into
+// coherent pinned memory after a system-scope fence: spin on it, then the
+// batch's end event), check it and hand first[] to the caller.
+int Engine::fast_collect(int k) {
+    FastBatch &b = fb_[k];
+    if (!b.resolved) {
+        set_error("internal: FastCDC batch collected before its resolve was enqueued");
+        return CDC_EDEVICE;
+    }
+    uint64_t *h_misc = fs_[b.slot].h + 4 * h_stage_streams_;
     {
         const volatile uint64_t *done = h_misc + p3::kStatDone;
-        const auto budget = std::chrono::microseconds(
-            std::min<uint64_t>(2000, std::max<uint64_t>(100, timing_.bytes / 2000000)));
+        const auto budget =
+            std::chrono::microseconds(std::min<uint64_t>(2000, std::max<uint64_t>(100, b.bytes / 2000000)));
         const auto t_spin = std::chrono::steady_clock::now();
         while (*done == ~0ull && std::chrono::steady_clock::now() - t_spin < budget) __builtin_ia32_pause();
     }
-    // Once the done word is set every block has written its output (each
-    // fences before taking its ticket; the last one fences system-wide before
-    // the word): the results are complete and the call returns without
-    // waiting for the kernel to retire.  Work the caller queues on this
-    // stream stays ordered after it; the events are read on request (timing()).
-    const bool seen = h_misc[p3::kStatDone] != ~0ull;
-    if (!seen) HIP_TRY(hipStreamSynchronize(s));
+    if (h_misc[p3::kStatDone] == ~0ull) HIP_TRY(hipEventSynchronize(tev_[b.seq % kTimeRing][2]));
+    b.live = false;
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
         set_error(h_misc[p3::kStatDone] != 1 ? "resolve kernel did not report back"
                                              : "chain overflow, output bound or look-back timeout (internal error)");
         return CDC_EDEVICE;
     }
     if (fp_.diag & 128) {
-        const double waves = (double)p3::resolve_blocks(st.total_spans) * 4;
-        std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk lookback(w0) out):");
+        const double units = b.ra.units ? (double)b.ra.units : 1.0;
+        std::fprintf(stderr, "resolve phases, us per unit (meta recs settle+wait virtual-links record-links walk "
+                             "lookback out):");
         for (int i = 0; i < p3::kStatDiagN; ++i)
-            std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / waves);
+            std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / units);
         std::fprintf(stderr, "\n");
     }
     // Zero-length streams own no span: their first[] is the next stream's.
-    const uint64_t *lens = static_cast<uint64_t *>(h_stage_) + h_stage_streams_;
+    const uint64_t *lens = fs_[b.slot].h + h_stage_streams_;
     uint64_t *hf = h_misc + p3::kStatWords;
-    for (size_t i = n; i-- > 0;)
+    for (size_t i = b.n; i-- > 0;)
         if (lens[i] == 0) hf[i] = hf[i + 1];
-    std::memcpy(first, hf, (n + 1) * 8);
-    timing_pending_ = true;
-    if (!seen) (void)timing();
-    timing_.compact_ms = 0;  // fused into the resolve kernel
+    std::memcpy(b.first, hf, (b.n + 1) * 8);
+    const double hash_ms = timing_.hash_ms;
+    timing_ = cdc_timing_t{};
+    timing_.hash_ms = hash_ms;
+    timing_.bytes = b.bytes;
     timing_.candidates = h_misc[p3::kStatCand];
     timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
     timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk];
     timing_.walk_fallback_steps = h_misc[p3::kStatOnDemand];
+    timing_pending_ = true;
+    timing_seq_ = b.seq;
     return CDC_OK;
 }
 
@@ -596,15 +780,20 @@ int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, siz
     return CDC_OK;
 }
 
+// FastCDC batch events: [0] before its scan launch, [1] after it, [2] after
+// the launch that resolved it -- the next batch's scan launch when batches
+// are pipelined (so resolve_ms then also spans that scan), or its own resolve.
 const cdc_timing_t &Engine::timing() {
+    if (fb_any_) (void)fast_drain();
     if (timing_pending_) {
         timing_pending_ = false;
-        (void)timing_back(0, timing_);
+        (void)timing_back((uint32_t)(fast_batches_ - 1 - timing_seq_), timing_);
     }
     return timing_;
 }
 
 int Engine::timing_back(uint32_t back, cdc_timing_t &out) {
+    if (fb_any_) (void)fast_drain();
     if (algo_ != CDC_ALGO_FASTCDC || back >= kTimeRing || back >= fast_batches_) {
         set_error("cdc_debug_timing_back: no such FastCDC batch in the event ring");
         return CDC_EINVAL;
@@ -677,6 +866,10 @@ int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, si
         return CDC_EINVAL;
     }
     HIP_TRY(hipSetDevice(device_));
+    if (fb_any_) {  // (the chunks it hashes are usually the last batch's)
+        const int64_t r = fast_drain();
+        if (r < 0) return (int)r;
+    }
     hipStream_t st = s ? s : own_stream_;
     (void)timing();  // the last batch's events, before ev_[2] is re-recorded
     HIP_TRY(hipEventRecord(ev_[3], st));
@@ -690,6 +883,10 @@ int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, si
 }
 
 int64_t Engine::debug_copy(int what, void *out, size_t max_bytes) {
+    if (fb_any_) {
+        const int64_t r = fast_drain();
+        if (r < 0) return r;
+    }
     if (algo_ != CDC_ALGO_FASTCDC || !ws_) {
         set_error("debug_copy: no FastCDC batch yet");
         return CDC_EINVAL;
@@ -711,6 +908,32 @@ int64_t Engine::debug_copy(int what, void *out, size_t max_bytes) {
     HIP_TRY(hipStreamSynchronize(own_stream_));
     if (bytes) HIP_TRY(hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost));
     return (int64_t)bytes;
+}
+
+int Engine::read_bw(const uint8_t *d_buf, size_t len, int reps, double *ms) {
+    HIP_TRY(hipSetDevice(device_));
+    if (fb_any_) {
+        const int64_t r = fast_drain();
+        if (r < 0) return (int)r;
+    }
+    uint64_t *d_acc = nullptr;
+    const size_t words = (size_t)num_cus_ * 8;
+    HIP_TRY(hipMalloc(&d_acc, words * 8));
+    hipError_t e = hipMemsetAsync(d_acc, 0, words * 8, own_stream_);
+    if (e == hipSuccess) e = launch_read_reduce(d_buf, len, d_acc, num_cus_, own_stream_);  // (warm-up)
+    if (e == hipSuccess) e = hipEventRecord(ev_[0], own_stream_);
+    for (int r = 0; e == hipSuccess && r < reps; ++r) e = launch_read_reduce(d_buf, len, d_acc, num_cus_, own_stream_);
+    if (e == hipSuccess) e = hipEventRecord(ev_[3], own_stream_);
+    if (e == hipSuccess) e = hipEventSynchronize(ev_[3]);
+    float t = 0;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, ev_[0], ev_[3]);
+    (void)hipFree(d_acc);
+    if (e != hipSuccess) {
+        set_error(std::string("read_bw: ") + hipGetErrorString(e));
+        return CDC_EDEVICE;
+    }
+    *ms = (double)t / reps;
+    return CDC_OK;
 }
 
 int Engine::fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s) {

@@ -96,6 +96,14 @@ class Engine {
     int64_t chunk_batch_device(size_t n, const uint8_t *const *d_streams,
                                const uint64_t *lens, cdc_chunk_t *d_out,
                                size_t out_cap, uint64_t *first, hipStream_t stream);
+    // The same, enqueued (cdc_chunk_batch_device_async): FastCDC batches are
+    // pipelined -- the scan launch of batch k also resolves batch k-1 -- and
+    // first[] is filled by batch_sync().  Other algorithms run synchronously.
+    int64_t chunk_batch_device_async(size_t n, const uint8_t *const *d_streams, const uint64_t *lens,
+                                     cdc_chunk_t *d_out, size_t out_cap, uint64_t *first, hipStream_t stream);
+    // Waits for every enqueued batch (resolving the last one); the total chunk
+    // count of the last batch, or a negative code.
+    int64_t batch_sync();
     size_t estimate(size_t len) const;
     // Strict bound: every FastCDC chunk but the last is >= 2*(min/2) bytes
     // (cut_gear starts testing at index 2*(min/2)).
@@ -115,6 +123,7 @@ class Engine {
     cdc_algo_t algo() const { return algo_; }
     int device() const { return device_; }
     int fill_splitmix64(uint8_t *d_buf, size_t len, uint64_t seed, hipStream_t s);
+    int read_bw(const uint8_t *d_buf, size_t len, int reps, double *ms);
     // Debug (include/chunkfs_amd_debug.h): copy an intermediate array of the
     // last FastCDC batch to the host.  what: 0 = per-span candidate counts
     // (u32), 1 = candidate records (u32, cap per span).  Returns bytes copied.
@@ -129,8 +138,16 @@ class Engine {
     int init();
     int ensure_workspace(uint64_t spans, size_t n);
     int ensure_host_staging(size_t n);
-    int run_fast(const StreamTable &st, cdc_chunk_t *d_out, size_t n,
-                 uint64_t *first, hipStream_t s);
+    // FastCDC regular pipeline: enqueue the scan of a batch (fused with the
+    // resolve of the pending previous one), the standalone resolve of the last
+    // one, and the collection of a batch's results.
+    int64_t batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
+                         size_t out_cap, uint64_t *first, hipStream_t stream, bool async);
+    int64_t fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
+                        size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s);
+    int fast_resolve_pending();
+    int fast_collect(int rec);
+    int64_t fast_drain();
     // One small FastCDC stream in one launch (small.hip): CDC_OK, kSmallFallback
     // (a budget was exceeded: run the regular pipeline) or a CDC_E* code.
     static constexpr int kSmallFallback = 1;
@@ -185,12 +202,39 @@ class Engine {
     size_t ws_bytes_ = 0;
     uint64_t ws_spans_ = 0;
     size_t ws_streams_ = 0;
-    Candidates cand_{};
+    Candidates cand_{};            // the last FastCDC batch's (debug_copy)
     p3::Chains ch3_{};             // chunk starts spilled past the resolve's LDS
-    p3::Compact cp3_{};
     p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
     uint64_t res_gen_ = 0;
-    uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids
+    uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids (walk engine: unused)
+    uint64_t *d_part_ = nullptr;   // resolve: per-block statistics
+    // FastCDC buffers of two batches in flight (slot = sequence number % 2):
+    // what the scan of batch k writes while the resolve of batch k-1 reads.
+    static constexpr int kSlots = 2;
+    struct FastSlot {
+        Candidates cand{};
+        const uint8_t **d_ptrs = nullptr;
+        uint64_t *d_lens = nullptr, *d_sb = nullptr, *d_tails = nullptr, *stats = nullptr;
+        uint64_t *h = nullptr;           // pinned staging: ptrs, lens, span_base, tails, stats ++ first
+        std::vector<uint64_t> tables;    // ptrs ++ lens as last uploaded (skip the H2D when unchanged)
+        uint64_t tables_gen = ~0ull;
+        uint32_t n_tails = 0;            // ragged last spans of those tables
+    } fs_[kSlots];
+    // Batches in flight, by sequence number % 3: batch k is scanned by launch
+    // k, resolved by launch k+1 (or its own resolve launch) and collected
+    // before launch k+2 reuses its host stats block.
+    struct FastBatch {
+        bool live = false, resolved = false;
+        int slot = 0;
+        size_t n = 0;
+        uint64_t *first = nullptr;  // the caller's first[n+1]
+        p3::ResArgs ra{};
+        uint64_t seq = 0, bytes = 0;
+    } fb_[3];
+    uint64_t timing_seq_ = 0;       // the batch timing_ describes
+    uint64_t fb_seq_ = 0;           // batches submitted
+    hipStream_t fb_stream_ = nullptr;  // the stream of the batches in flight
+    bool fb_any_ = false;           // a batch is in flight
     const uint64_t *cur_tails_ = nullptr;  // this batch's: d_tails_ or the staging block's
     uint32_t n_tails_ = 0;
     uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
@@ -201,7 +245,7 @@ class Engine {
     // Pinned, device-visible (coherent) host staging: the small per-call
     // tables going in, stats ++ first[n+1] coming back (written by the
     // resolve kernel directly, no copy).
-    void *h_stage_ = nullptr;
+    void *h_stage_ = nullptr;       // slot 0 (the small and walk paths use its layout too), then slot 1
     size_t h_stage_streams_ = 0;
 
     // Host path (hostpath.cpp): pinned upload ring (slot k reused once its

@@ -39,7 +39,32 @@ __global__ void fill_kernel(uint8_t *buf, uint64_t len, uint64_t seed) {
     }
 }
 
+// Read-only reduction (the measured-achievable HBM read rate the FastCDC scan
+// is compared with): every byte read once with 16-byte
+// coalesced loads, four in flight per lane, XOR-folded; one word per block.
+__global__ __launch_bounds__(256) void read_kernel(const uint4 *__restrict__ p, uint64_t n16, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) {
+        const uint4 a = p[i];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
+    if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned int *>(out + blockIdx.x), acc);
+}
+
 }  // namespace
+
+hipError_t launch_read_reduce(const uint8_t *d_buf, uint64_t len, uint64_t *d_out, int num_cus, hipStream_t s) {
+    if (len < 16) return hipSuccess;
+    read_kernel<<<(unsigned)(num_cus * 8), 256, 0, s>>>(reinterpret_cast<const uint4 *>(d_buf), len / 16, d_out);
+    return hipGetLastError();
+}
 
 hipError_t launch_fixed(const StreamTable &st, uint64_t chunk_size, const uint64_t *d_first, void *d_out,
                         uint64_t total, hipStream_t s) {

@@ -144,6 +144,27 @@ int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
                                size_t out_cap, uint64_t *first,
                                void *hip_stream);
 
+/* The same batch, enqueued: returns 0 once the batch is submitted, and
+ * `first` (kept by the library until then) is filled by cdc_batch_sync.
+ * FastCDC batches of more than 8 MiB are pipelined on the device: the scan
+ * launch of batch k also resolves batch k-1 (the resolve waves run beside the
+ * scan waves), so back-to-back batches pay the resolve off the critical
+ * path; d_streams' bytes and d_out must stay untouched until cdc_batch_sync.
+ * Consecutive async batches of one handle must use one hip_stream (another
+ * stream first completes the batches in flight).  Smaller FastCDC batches
+ * and other algorithms complete inside this call (first filled on return).
+ * Any other call on the handle first completes the batches in flight. */
+int64_t cdc_chunk_batch_device_async(cdc_handle_t *h, size_t n,
+                                     const uint8_t *const *d_streams,
+                                     const uint64_t *lens, cdc_chunk_t *d_out,
+                                     size_t out_cap, uint64_t *first,
+                                     void *hip_stream);
+
+/* Completes every batch enqueued by cdc_chunk_batch_device_async (their
+ * first[] arrays are filled); returns the last batch's total chunk count (0
+ * when none was in flight) or a negative code. */
+int64_t cdc_batch_sync(cdc_handle_t *h);
+
 size_t cdc_batch_max_chunks(const cdc_handle_t *h, size_t n,
                             const uint64_t *lens);
 

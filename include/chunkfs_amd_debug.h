@@ -38,6 +38,12 @@ int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n);
  * after the loop instead of waiting on each batch's events inside it.
  * CDC_EINVAL when that batch is not in the ring. */
 int cdc_debug_timing_back(cdc_handle_t *h, uint32_t back, cdc_timing_t *t, size_t t_size);
+/* Measured-achievable HBM read rate on the handle's device: a read-only
+ * reduction kernel (16-byte coalesced loads, every byte once) over the DEVICE
+ * buffer d_buf[len], `reps` timed launches after one warm-up; *ms = the
+ * average launch time (HIP events).  The denominator of the bench line's
+ * roofline.frac_of_achievable. */
+int cdc_debug_read_bw(cdc_handle_t *h, const uint8_t *d_buf, size_t len, int reps, double *ms);
 
 #ifdef __cplusplus
 }
