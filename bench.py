@@ -165,8 +165,8 @@ class DeviceEngine:
 
     def step(self, w):
         """Enqueue one pass (cdc_chunk_batch_device_async): back-to-back FastCDC
-        batches are pipelined -- the scan launch of step k also resolves step
-        k-1 -- and sync() completes them; the returned first[] is filled then."""
+        batches run with no host round trip between them, and sync() completes
+        them; the returned first[] is filled then."""
         return self.ch.chunk_batch_device_async(w.ptrs_a, w.lens_a, w.out.data_ptr(), w.cap)
 
     def timing(self):
@@ -958,7 +958,7 @@ def main(argv=None):
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "scan_kernel (gear candidate scan; its launch also resolves the previous step)",
+                "kernel": "scan_kernel (gear candidate scan)",
                 "kernel_ms": scan_avg_ms, "algorithmic_bytes_per_launch": bytes_rank,
                 "achievable_GBps": read_gbs,
                 "frac_of_achievable": (achieved / read_gbs) if (achieved and read_gbs) else None,

@@ -190,8 +190,8 @@ class Chunker:
 
     def chunk_batch_device_async(self, d_ptrs, lens, d_out_ptr, out_cap, stream=0):
         """cdc_chunk_batch_device_async: enqueue the batch (FastCDC batches of
-        more than 8 MiB are pipelined: the next batch's scan launch resolves
-        it).  Returns its first[n+1] array, filled by batch_sync()."""
+        more than 8 MiB run back to back with no host wait between them).
+        Returns its first[n+1] array, filled by batch_sync()."""
         ptrs = np.ascontiguousarray(np.asarray(d_ptrs, dtype=np.uint64))
         lens_a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
         n = int(lens_a.size)

@@ -261,14 +261,11 @@ int Engine::ensure_host_staging(size_t n) {
     // Per slot: ptrs[W] lens[W] span_base[W] tails[W] | stats ++ first[n+1]
     // (fixed: first[n+1]) -- stream tables 4 n, device-written stats / flags
     // ++ first[n+1] (n + 32), the walk's flags[4] and fix-up round flag blocks
-    // (4 x walk::kMaxFixRounds).  Slot 1: the second FastCDC batch in flight.
-    const size_t per = 5 * want + 36 + 4 * walk::kMaxFixRounds;
-    HIP_TRY(hipHostMalloc(&h_stage_, kSlots * per * sizeof(uint64_t), hipHostMallocCoherent));
+    // (4 x walk::kMaxFixRounds).  Slots 1-2: more FastCDC batches in flight.
+    h_stage_per_ = 5 * want + 36 + 4 * walk::kMaxFixRounds;
+    HIP_TRY(hipHostMalloc(&h_stage_, kHostSlots * h_stage_per_ * sizeof(uint64_t), hipHostMallocCoherent));
     h_stage_streams_ = want;
-    for (int k = 0; k < kSlots; ++k) {
-        fs_[k].h = static_cast<uint64_t *>(h_stage_) + k * per;
-        fs_[k].tables.clear();
-    }
+    for (int k = 0; k < kSlots; ++k) fs_[k].tables.clear();
     return CDC_OK;
 }
 
@@ -302,9 +299,8 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     }
     const size_t o_starts = take(S * smax * 8);  // chunk starts beyond the LDS-resident ones
     const size_t o_first = take((N + 1) * 8);
-    const uint64_t nb = p3::resolve_units(S) + 2;
+    const uint64_t nb = p3::resolve_blocks(S) + 2;
     const size_t o_desc = take(6 * nb * 8);
-    const size_t o_part = take((size_t)p3::resolve_part_words(num_cus_) * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
     ws_spans_ = 0;
@@ -338,7 +334,6 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     rs3_ = p3::Resolve{desc, desc + nb, desc + 2 * nb, desc + 3 * nb, desc + 4 * nb, desc + 5 * nb, 0};
     HIP_TRY(hipMemset(desc, 0, 6 * nb * 8));  // no stale status word can carry a live generation
     d_tails_ = fs_[0].d_tails;
-    d_part_ = reinterpret_cast<uint64_t *>(b + o_part);
     return CDC_OK;
 }
 
@@ -472,9 +467,9 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
     return (int64_t)first[n];
 }
 
-// One FastCDC batch into the pipeline: its tables into the batch's slot, then
-// ONE launch that scans it and resolves the pending previous batch (if any).
-// The batch itself is resolved by the next submit's launch or by fast_drain().
+// One FastCDC batch enqueued: its tables into the batch's slots, the scan and
+// the resolve launches; no host wait.  The host collects it (fast_collect)
+// when its stats block is needed again or at fast_drain().
 int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
                             size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s) {
     if (fb_any_ && s != fb_stream_) {  // one pipeline per stream
@@ -491,7 +486,7 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
         if (r < 0) return r;
     }
     const uint64_t seq = fb_seq_;
-    if (fb_[seq % 3].live) {  // batch seq-3: the stats block this launch's resolve writes next
+    if (fb_[seq % 3].live) {  // batch seq-3: its host block is this batch's
         const int rc = fast_collect((int)(seq % 3));
         if (rc) {
             (void)fast_drain();
@@ -504,14 +499,15 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     if (rc) return rc;
     const int slot = (int)(seq % kSlots);
     FastSlot &f = fs_[slot];
-    uint64_t *h_ptrs = f.h, *h_lens = f.h + h_stage_streams_, *h_sb = f.h + 2 * h_stage_streams_;
-    uint64_t *h_tails = f.h + 3 * h_stage_streams_;
+    uint64_t *hb = static_cast<uint64_t *>(h_stage_) + (seq % kHostSlots) * h_stage_per_;
+    uint64_t *h_ptrs = hb, *h_lens = hb + h_stage_streams_, *h_sb = hb + 2 * h_stage_streams_;
+    uint64_t *h_tails = hb + 3 * h_stage_streams_;
     bool same = !zero_copy && f.tables_gen == ws_gen_ && f.tables.size() == 2 * n;
     for (size_t i = 0; same && i < n; ++i)
         same = f.tables[i] == reinterpret_cast<uint64_t>(d_streams[i]) && f.tables[n + i] == lens[i];
-    if (!same) {
-        // (the slot's previous H2D copies ran before the launch two batches
-        // back, which was collected or is ahead of this one on the stream)
+    {
+        // this batch's tables in its own host block (its collection reads the
+        // lengths); the device slot's copies are re-uploaded when they differ
         uint64_t sp = 0;
         uint32_t nt = 0;
         for (size_t i = 0; i < n; ++i) {
@@ -522,13 +518,16 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
             if (lens[i] & ((1ull << sl2) - 1)) h_tails[nt++] = sp - 1;  // ragged last span
         }
         h_sb[n] = sp;
+        if (same && nt != f.n_tails) same = false;  // (cannot differ for equal tables; a guard)
         f.n_tails = nt;
+    }
+    if (!same) {
         f.tables.clear();
         if (!zero_copy) {
             HIP_TRY(hipMemcpyAsync(f.d_ptrs, h_ptrs, n * 8, hipMemcpyHostToDevice, s));
             HIP_TRY(hipMemcpyAsync(f.d_lens, h_lens, n * 8, hipMemcpyHostToDevice, s));
             HIP_TRY(hipMemcpyAsync(f.d_sb, h_sb, (n + 1) * 8, hipMemcpyHostToDevice, s));
-            if (nt) HIP_TRY(hipMemcpyAsync(f.d_tails, h_tails, nt * 8, hipMemcpyHostToDevice, s));
+            if (f.n_tails) HIP_TRY(hipMemcpyAsync(f.d_tails, h_tails, f.n_tails * 8, hipMemcpyHostToDevice, s));
             f.tables.assign(h_ptrs, h_ptrs + n);
             f.tables.insert(f.tables.end(), h_lens, h_lens + n);
             f.tables_gen = ws_gen_;
@@ -541,7 +540,7 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     st.n = (uint32_t)n;
     st.span_log2 = sl2;
     st.total_spans = spans;
-    uint64_t *h_misc = f.h + 4 * h_stage_streams_;  // stats ++ first[n+1], written by the device
+    uint64_t *h_misc = hb + 4 * h_stage_streams_;  // stats ++ first[n+1], written by the device
     const p3::Compact cp{f.stats, h_misc, h_misc + p3::kStatWords};
     h_misc[p3::kStatDone] = ~0ull;  // sentinel: overwritten by the resolve's last block
     if (!spans) {  // every stream is empty: nothing to launch
@@ -551,35 +550,25 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     }
     p3::Resolve rs = rs3_;
     rs.gen = ++res_gen_;
-    FastBatch *prev = nullptr;
-    if (fb_any_) {
-        FastBatch &pb = fb_[(seq + 2) % 3];  // batch seq-1
-        if (pb.live && !pb.resolved) prev = &pb;
-    }
     FastBatch &rec = fb_[seq % 3];
     rec = FastBatch{};
     rec.live = true;
-    rec.resolved = spans == 0;
+    rec.resolved = true;
     rec.slot = slot;
+    rec.h = hb;
     rec.n = n;
     rec.first = first;
     rec.seq = seq;
     rec.bytes = bytes;
-    rec.ra = p3::ResArgs{st, f.cand, ch3_, cp, rs, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap,
-                         p3::resolve_units(spans), d_part_};
+    rec.spans = spans;
     hipEvent_t *ev = tev_[seq % kTimeRing];
     HIP_TRY(hipEventRecord(ev[0], s));
-    if (spans || prev) {
-        const p3::ResArgs none{};
-        HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails,
-                                num_cus_, prev ? prev->ra : none, s));
-    }
+    if (spans)
+        HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails, num_cus_,
+                                s));
     HIP_TRY(hipEventRecord(ev[1], s));
-    if (prev) {
-        prev->resolved = true;
-        HIP_TRY(hipEventRecord(tev_[prev->seq % kTimeRing][2], s));
-    }
-    if (rec.resolved) HIP_TRY(hipEventRecord(ev[2], s));
+    if (spans) HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, s));
+    HIP_TRY(hipEventRecord(ev[2], s));
     fb_seq_ = seq + 1;
     fast_batches_ = fb_seq_;
     fb_any_ = true;
@@ -589,22 +578,12 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     return 0;
 }
 
-// The last batch's resolve on its own, then every batch in flight collected
-// in order.  Returns the last batch's chunk count.
+// Every batch in flight collected in order.  Returns the last batch's chunk
+// count.
 int64_t Engine::fast_drain() {
     if (!fb_any_) return 0;
     const uint64_t last = fb_seq_ - 1;
-    FastBatch &lb = fb_[last % 3];
     int rc = CDC_OK;
-    if (lb.live && !lb.resolved) {
-        lb.resolved = true;
-        const hipError_t e = p3::launch_resolve(lb.ra, fp_, d_gear_, num_cus_, fb_stream_);
-        if (e != hipSuccess) {
-            set_error(std::string("launch_resolve: ") + hipGetErrorString(e));
-            rc = CDC_EDEVICE;
-        }
-        (void)hipEventRecord(tev_[lb.seq % kTimeRing][2], fb_stream_);
-    }
     int64_t total = 0;
     for (uint64_t q = last >= 2 ? last - 2 : 0; q <= last; ++q) {
         FastBatch &b = fb_[q % 3];
@@ -628,7 +607,7 @@ int Engine::fast_collect(int k) {
         set_error("internal: FastCDC batch collected before its resolve was enqueued");
         return CDC_EDEVICE;
     }
-    uint64_t *h_misc = fs_[b.slot].h + 4 * h_stage_streams_;
+    uint64_t *h_misc = b.h + 4 * h_stage_streams_;
     {
         const volatile uint64_t *done = h_misc + p3::kStatDone;
         const auto budget =
@@ -644,15 +623,15 @@ int Engine::fast_collect(int k) {
         return CDC_EDEVICE;
     }
     if (fp_.diag & 128) {
-        const double units = b.ra.units ? (double)b.ra.units : 1.0;
-        std::fprintf(stderr, "resolve phases, us per unit (meta recs settle+wait virtual-links record-links walk "
-                             "lookback out):");
+        const double waves = (double)p3::resolve_blocks(b.spans) * 8;
+        std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk "
+                             "lookback(w0) out):");
         for (int i = 0; i < p3::kStatDiagN; ++i)
-            std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / units);
+            std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / (waves ? waves : 1.0));
         std::fprintf(stderr, "\n");
     }
     // Zero-length streams own no span: their first[] is the next stream's.
-    const uint64_t *lens = fs_[b.slot].h + h_stage_streams_;
+    const uint64_t *lens = b.h + h_stage_streams_;
     uint64_t *hf = h_misc + p3::kStatWords;
     for (size_t i = b.n; i-- > 0;)
         if (lens[i] == 0) hf[i] = hf[i + 1];
@@ -780,9 +759,8 @@ int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, siz
     return CDC_OK;
 }
 
-// FastCDC batch events: [0] before its scan launch, [1] after it, [2] after
-// the launch that resolved it -- the next batch's scan launch when batches
-// are pipelined (so resolve_ms then also spans that scan), or its own resolve.
+// FastCDC batch events: [0] before its scan launch, [1] after it (before the
+// resolve), [2] after the resolve.
 const cdc_timing_t &Engine::timing() {
     if (fb_any_) (void)fast_drain();
     if (timing_pending_) {

@@ -96,9 +96,9 @@ class Engine {
     int64_t chunk_batch_device(size_t n, const uint8_t *const *d_streams,
                                const uint64_t *lens, cdc_chunk_t *d_out,
                                size_t out_cap, uint64_t *first, hipStream_t stream);
-    // The same, enqueued (cdc_chunk_batch_device_async): FastCDC batches are
-    // pipelined -- the scan launch of batch k also resolves batch k-1 -- and
-    // first[] is filled by batch_sync().  Other algorithms run synchronously.
+    // The same, enqueued (cdc_chunk_batch_device_async): FastCDC batches of
+    // more than 8 MiB go back to back on the stream with no host wait, first[]
+    // filled by batch_sync().  Other algorithms run synchronously.
     int64_t chunk_batch_device_async(size_t n, const uint8_t *const *d_streams, const uint64_t *lens,
                                      cdc_chunk_t *d_out, size_t out_cap, uint64_t *first, hipStream_t stream);
     // Waits for every enqueued batch (resolving the last one); the total chunk
@@ -138,14 +138,12 @@ class Engine {
     int init();
     int ensure_workspace(uint64_t spans, size_t n);
     int ensure_host_staging(size_t n);
-    // FastCDC regular pipeline: enqueue the scan of a batch (fused with the
-    // resolve of the pending previous one), the standalone resolve of the last
-    // one, and the collection of a batch's results.
+    // FastCDC regular pipeline: enqueue a batch (scan + resolve), collect a
+    // batch's results, drain every batch in flight.
     int64_t batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
                          size_t out_cap, uint64_t *first, hipStream_t stream, bool async);
     int64_t fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
                         size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s);
-    int fast_resolve_pending();
     int fast_collect(int rec);
     int64_t fast_drain();
     // One small FastCDC stream in one launch (small.hip): CDC_OK, kSmallFallback
@@ -207,29 +205,31 @@ class Engine {
     p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
     uint64_t res_gen_ = 0;
     uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids (walk engine: unused)
-    uint64_t *d_part_ = nullptr;   // resolve: per-block statistics
-    // FastCDC buffers of two batches in flight (slot = sequence number % 2):
-    // what the scan of batch k writes while the resolve of batch k-1 reads.
-    static constexpr int kSlots = 2;
+    // FastCDC batches in flight: device tables and candidates in two slots
+    // (slot = sequence number % 2; stream order protects them) whose uploaded
+    // tables are kept to skip unchanged H2D copies; host staging in three
+    // slots (batch record k % 3, below): batch k's block -- tables going in,
+    // stats ++ first[] coming back -- is read at its collection, before
+    // submit k+3 reuses it.
+    static constexpr int kSlots = 2, kHostSlots = 3;
     struct FastSlot {
         Candidates cand{};
         const uint8_t **d_ptrs = nullptr;
         uint64_t *d_lens = nullptr, *d_sb = nullptr, *d_tails = nullptr, *stats = nullptr;
-        uint64_t *h = nullptr;           // pinned staging: ptrs, lens, span_base, tails, stats ++ first
         std::vector<uint64_t> tables;    // ptrs ++ lens as last uploaded (skip the H2D when unchanged)
         uint64_t tables_gen = ~0ull;
         uint32_t n_tails = 0;            // ragged last spans of those tables
     } fs_[kSlots];
-    // Batches in flight, by sequence number % 3: batch k is scanned by launch
-    // k, resolved by launch k+1 (or its own resolve launch) and collected
-    // before launch k+2 reuses its host stats block.
+    // Batches in flight, by sequence number % 3 (cdc_chunk_batch_device_async):
+    // scan + resolve enqueued at submit, collected (done word, first[]) by the
+    // submit three later or by fast_drain.
     struct FastBatch {
         bool live = false, resolved = false;
-        int slot = 0;
+        int slot = 0;                // device slot
+        uint64_t *h = nullptr;       // host staging block (slot seq % kHostSlots)
         size_t n = 0;
         uint64_t *first = nullptr;  // the caller's first[n+1]
-        p3::ResArgs ra{};
-        uint64_t seq = 0, bytes = 0;
+        uint64_t seq = 0, bytes = 0, spans = 0;
     } fb_[3];
     uint64_t timing_seq_ = 0;       // the batch timing_ describes
     uint64_t fb_seq_ = 0;           // batches submitted
@@ -245,8 +245,8 @@ class Engine {
     // Pinned, device-visible (coherent) host staging: the small per-call
     // tables going in, stats ++ first[n+1] coming back (written by the
     // resolve kernel directly, no copy).
-    void *h_stage_ = nullptr;       // slot 0 (the small and walk paths use its layout too), then slot 1
-    size_t h_stage_streams_ = 0;
+    void *h_stage_ = nullptr;       // slot 0 (the small and walk paths use its layout too), then slots 1-2
+    size_t h_stage_streams_ = 0, h_stage_per_ = 0;
 
     // Host path (hostpath.cpp): pinned upload ring (slot k reused once its
     // DMA event completes), host-mapped chunk output written by the kernels,

@@ -65,7 +65,7 @@ __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
 #define SCHED_FENCE() do {} while (0)
 #endif
 #ifndef CDC_SCAN_WAVES
-#define CDC_SCAN_WAVES 12
+#define CDC_SCAN_WAVES 12  // as fast as 16 (profiles/r05/r05v_scan_12_waves.log), 136 KiB of LDS
 #endif
 #ifndef CDC_SCAN_LOOK
 #define CDC_SCAN_LOOK 1
@@ -526,6 +526,130 @@ struct ScanLds {
     uint32_t ecnt[kW][kEntCap];
 };
 
+// Full spans.  Lane l owns the contiguous segment [l*sub, (l+1)*sub) and
+// hashes it serially from hash 0; its first 48 positions are re-tested at the
+// end with the true carry-in (lane l-1's final hash, one DPP shift; lane 0's
+// from the 48 bytes before the span).  Ragged last spans: scan_tail_kernel.
+template <bool kAlign, int kW, int kLook, int kMode>
+__global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, const FastParams fp,
+                                                           const uint64_t *__restrict__ gear,
+                                                           const Candidates cand, const Compact cp) {
+    __shared__ ScanLds<kW> L;
+    const uint64_t *tab = L.tab;
+    for (int i = threadIdx.x; i < 256 * kCopies; i += kW * 64)
+        L.tab[i] = gear[i / kCopies] << fp.tshift;  // pre-shifted GEAR (see FastParams)
+    if (blockIdx.x == 0 && threadIdx.x < kStatWords) cp.stats[threadIdx.x] = 0;  // the resolve accumulates
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t rep = (lane & 31) * 8;  // this lane's GEAR replica
+    const uint64_t span = 1ull << st.span_log2;
+    const uint32_t sub_log2 = st.span_log2 - 6;
+    const uint32_t sub = 1u << sub_log2;   // bytes per lane per span (>= 1 KiB)
+    const uint32_t steps = sub / kStep;    // >= 16, a power of two
+    const uint32_t lo = lane << sub_log2;  // lane's first byte in the span
+    const uint64_t istride = 16ull * sub;
+    const EntryList E{L.epos[wave], L.ehlo[wave], L.ehhi[wave], L.ecnt[wave]};
+    // Instruction i's lane quad u = lane/4 loads row 16 i + rsel(u); the two
+    // quads of one ds_write_b128 lane group (8 lanes) get rows 4 apart, so
+    // their 80-byte rows sit 16 banks apart and the write is conflict-free
+    // (rows u, u+1 collided on one 4-bank group: 8 extra LDS cycles per
+    // store, r02av PMC); the reads (lane = row) are unchanged.
+    const uint32_t rsel = ((lane >> 3) & 3) + 8 * (lane >> 5) + 4 * ((lane >> 2) & 1);
+    uint4 *wrow = &L.stage[wave][rsel * 5 + (lane & 3)];
+    const uint4 *rrow = &L.stage[wave][lane * 5];
+
+    // Spans are software-pipelined: the first two steps of the next span are
+    // in flight while this span's fix-up and flush run.  Ragged last spans:
+    // scan_tail_kernel.
+    const uint64_t gstride = (uint64_t)gridDim.x * kW;
+    auto next_full = [&](uint64_t g, uint32_t &si, uint64_t &off) {
+        for (; g < st.total_spans; g += gstride) {
+            locate(st, g, si, off);
+            if (st.lens[si] - off >= span) break;
+        }
+        return g;
+    };
+    Q4 A, B, C;
+    uint32_t si, wb = 0;
+    uint64_t off;
+    uint64_t g = next_full((uint64_t)blockIdx.x * kW + wave, si, off);
+    const uint8_t *base = nullptr, *gp = nullptr;
+    auto prefetch = [&]() {  // first two steps and the carry bytes of span g
+        base = st.ptrs[si] + off;
+        gp = base + (uint64_t)rsel * sub + (lane & 3) * 16;
+        wb = 0;
+        if (off != 0 && lane < 48) wb = as_global1(base)[(int)lane - 48];
+        gload_step(A, gp, istride, 0);
+        SCHED_FENCE();
+        gload_step(B, gp, istride, 1);
+        SCHED_FENCE();
+    };
+    if (g < st.total_spans) prefetch();
+    while (g < st.total_spans) {
+        uint32_t ne = 0;  // quarter entries appended this span (wave-uniform)
+        uint64_t h = 0;
+        uint4 F0, F1, F2;
+        // Two steps in flight while one is hashed (A/B ring).  The loop body
+        // issues its loads unconditionally -- a conditional load leaves the
+        // compiler unsure how many are outstanding at the back edge, and it
+        // then waits for all of them -- so the last two steps are peeled.
+        stage_step(C, A, wrow, rrow);
+        F0 = C.q[0];
+        F1 = C.q[1];
+        F2 = C.q[2];
+        gload_step(A, gp, istride, 2);
+        SCHED_FENCE();
+// kMode: 0 = the scan; 1 = loads and transposes only, 2 = hashing only (timing
+// experiments: CHUNKFS_AMD_DIAG bits 8-9, results meaningless).
+#define CDC_PROC(POS)                                                                          \
+    do {                                                                                       \
+        if constexpr (kMode == 1) h ^= (uint64_t)(C.q[0].x ^ C.q[1].y ^ C.q[2].z ^ C.q[3].w);   \
+        else process_step<kAlign, kLook>(C, h, POS, ne, E, tab, rep, fp);                      \
+    } while (0)
+#define CDC_SCAN_PAIR(T, LOAD_B, STAGE_A, LOAD_A)                                              \
+    do {                                                                                       \
+        CDC_PROC(lo + (T) * kStep);                                                            \
+        SCHED_FENCE();                                                                         \
+        stage_step(C, B, wrow, rrow);                                                          \
+        if (LOAD_B && kMode != 2) gload_step(B, gp, istride, (T) + 3);                         \
+        SCHED_FENCE();                                                                         \
+        CDC_PROC(lo + ((T) + 1) * kStep);                                                      \
+        SCHED_FENCE();                                                                         \
+        if (STAGE_A) stage_step(C, A, wrow, rrow);                                             \
+        if (LOAD_A && kMode != 2) gload_step(A, gp, istride, (T) + 4);                         \
+        SCHED_FENCE();                                                                         \
+    } while (0)
+        uint32_t t = 0;
+        for (; t + 4 < steps; t += 2) CDC_SCAN_PAIR(t, true, true, true);
+        CDC_SCAN_PAIR(t, true, true, false);        // steps-4, steps-3
+        CDC_SCAN_PAIR(t + 2, false, false, false);  // steps-2, steps-1
+#undef CDC_SCAN_PAIR
+#undef CDC_PROC
+        // This span's carry-in bytes and identity, then the next span's prefetch.
+        const uint64_t g_cur = g, off_cur = off;
+        const uint64_t avail_cur = st.lens[si] - off;
+        const uint32_t wb_cur = wb;
+        const uint8_t *base_cur = base;
+        g = next_full(g + gstride, si, off);
+        if (g < st.total_spans) prefetch();
+        // Fix-up: re-test the first 48 positions with the true carry-in.
+        const uint64_t gw = lane < 48 ? L.tab[wb_cur * kCopies + (lane & 31)] : 0;
+        const uint64_t hw = readlane_u64(gear_prefix(gw, lane), 47);  // hash of the 48 bytes before
+        h = wave_shr1(h, off_cur != 0 ? hw : 0);
+        {
+            uint64_t h0 = h;
+            append_hits(quarter<kAlign>(h, F0, tab, rep, fp) == 0, lo | kEntFix, h0, ne, E);
+            h0 = h;
+            append_hits(quarter<kAlign>(h, F1, tab, rep, fp) == 0, (lo + 16) | kEntFix, h0, ne, E);
+            h0 = h;
+            append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, (lo + 32) | kEntFix, h0, ne, E);
+        }
+        flush_span(g_cur, base_cur, (uint32_t)span, avail_cur, sub - 1, ne, E, tab, rep, fp, cand, lane);
+    }
+}
+
 // ---- scan, LDS-DMA input landing (A/B path: CHUNKFS_AMD_DIAG bit 10) ---------
 //
 // The same scan with the bytes landed by global_load_lds_dwordx4 straight into
@@ -855,21 +979,17 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 // <= 47 "truncated" positions s+a0 .. s+a0+46, which are tested exactly from
 // the bytes; every later position comes from the scan's records.
 
-// Resolve units: a team of kTeam waves resolves kTeamSpans consecutive spans
-// (a "unit": each wave walks kWalkSpans of them) and publishes one look-back
-// descriptor.  Teams -- the blocks of the standalone resolve kernel, or the
-// resolve waves of the fused scan kernel's blocks (which resolve the previous
-// batch beside this batch's scan) -- claim units in dispatch order.  (Units of one wave measured
-// slower: 4096 descriptors per GiB made each look-back ~40 us,
-// profiles/r05/r05e_d128.log.)
+#ifndef CDC_RES_WAVES
+#define CDC_RES_WAVES 8  // 64 spans per block: one block per CU, all resident (r03q/r03r: 4 -> 8 waves, -7 us)
+#endif
 #ifndef CDC_WALK_SPANS
-#define CDC_WALK_SPANS 4
+#define CDC_WALK_SPANS 8
 #endif
 #ifndef CDC_WIN_RECS
-#define CDC_WIN_RECS 192
+#define CDC_WIN_RECS 768
 #endif
-constexpr int kTeam = 4;                  // resolve waves per block (one per SIMD)
-constexpr int kResThreads = kTeam * 64;   // standalone resolve kernel
+constexpr int kResWaves = CDC_RES_WAVES;
+constexpr int kResThreads = kResWaves * 64;
 
 // First hitting offset d in [0, tl-a0) of the truncated positions of the
 // chunk starting at c (hash reset at c+a0), or kTruncNone; w0 = c + a0.
@@ -950,6 +1070,11 @@ __device__ __noinline__ uint64_t coop_next_bytes(const FastParams fp, const uint
         h = __shfl(x, (int)(p1 - b - 1));
     }
     return s + R.rem;
+}
+
+__device__ __forceinline__ void load_tab1(uint64_t *tab, const uint64_t *gear) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) tab[i] = gear[i];
+    __syncthreads();
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
@@ -1042,8 +1167,8 @@ __device__ __forceinline__ void walk_lanes(const StreamTable &st, const FastPara
 
 // ---- resolve: window, links, walks, look-back --------------------------------
 //
-// One unit = kTeamSpans consecutive spans, resolved by a team of kTeam waves;
-// wave w walks kWalkSpans of them (lane l: span G0 + l) from a warm-up start
+// One block = kResWaves waves = kBlockSpans consecutive spans.  Wave w walks
+// kWalkSpans of them (lane l: span G0 + l), each from a warm-up start
 // kWarmSpans spans back, over links held in a compact per-wave LDS window:
 //   1. window metadata and every record of the window's kWinSlots spans, one
 //      batch of global loads;
@@ -1053,12 +1178,12 @@ __device__ __forceinline__ void walk_lanes(const StreamTable &st, const FastPara
 //      are not records (max cuts, truncated hits) become "virtual" entries,
 //      whose links are computed the same way from the bytes until none is new;
 //   4. the walks: LDS pointer chasing; the spans' chunk starts go to HBM;
-//   5. unit settle: a span whose entry differs from its predecessor's exit
+//   5. block settle: a span whose entry differs from its predecessor's exit
 //      is re-walked from that exit (rare; in order);
-//   6. decoupled look-back over units: the chunk-count prefix and the
-//      unit-boundary check (this unit's entry == the predecessor's exit).  A
-//      failed check waits for the unit at fault to publish its final state; a
-//      unit whose own entry is stale re-walks;
+//   6. decoupled look-back over blocks in dispatch order: the chunk-count
+//      prefix and the block-boundary check (this block's entry == the
+//      predecessor's exit).  A failed check waits for the block at fault to
+//      publish its final state; a block whose own entry is stale re-walks;
 //   7. Chunk{offset,length} at the final index, first[] and the statistics.
 constexpr int kWalkSpans = CDC_WALK_SPANS;
 #ifndef CDC_WARM_SPANS
@@ -1068,8 +1193,8 @@ constexpr int kWarmSpans = CDC_WARM_SPANS;
 constexpr int kWinSlots = kWarmSpans + kWalkSpans + 1;  // + 1: searched, never walked
 constexpr int kReach = kWarmSpans + kWalkSpans;         // slots whose records get links
 constexpr uint32_t kWinRecs = CDC_WIN_RECS;  // per-wave record budget (denser windows: global path)
-constexpr uint32_t kVirt = 48;      // virtual entries per wave (beyond: exact steps from the bytes)
-constexpr int kTeamSpans = kTeam * kWalkSpans;
+constexpr uint32_t kVirt = 128;     // virtual entries per wave
+constexpr int kBlockSpans = kResWaves * kWalkSpans;
 constexpr uint64_t kNoDep = ~0ull;  // block entry of a block that starts a stream
 constexpr uint64_t kAgg = 1, kInc = 2;
 constexpr uint32_t kSpinMax = 1u << 26;  // look-back poll bound: an error, never a hang
@@ -1097,19 +1222,15 @@ struct ChainWin {
     uint32_t nrec, nvirt;
 };
 
-struct TeamState {
-    uint64_t E[kTeamSpans];  // entry: first start >= span start
-    uint64_t X[kTeamSpans];  // exit: first start >= span end
-    uint32_t N[kTeamSpans];  // starts in the span
-    uint8_t F[kTeamSpans];   // 1: the span starts a stream
-    uint64_t base, pred;
+struct BlockState {
+    uint64_t E[kBlockSpans];  // entry: first start >= span start
+    uint64_t X[kBlockSpans];  // exit: first start >= span end
+    uint32_t N[kBlockSpans];  // starts in the span
+    uint8_t F[kBlockSpans];   // 1: the span starts a stream
+    uint64_t b, base, pred;
     uint32_t rewalk;
-};
-
-// A worker's statistics, summed per block at its end.
-struct UnitStats {
-    uint64_t cand = 0, rewalk = 0, steps = 0, err = 0;
-    uint64_t dt[kStatDiagN] = {};
+    uint64_t stat[kResWaves][3];  // per wave: candidates << 24 | overflowed, re-walks, exact steps
+    uint64_t diag[kResWaves][kStatDiagN];  // per wave phase times (diag & 128)
 };
 
 __device__ __forceinline__ uint64_t skey(uint32_t si) { return (uint64_t)si << kKeyShift; }
@@ -1237,7 +1358,7 @@ __device__ __forceinline__ void walk_window(ChainWin &W, const FastParams &fp, c
 __device__ __forceinline__ void wave_settle(const StreamTable &st, const FastParams &fp, const Candidates &cand,
                                             const uint64_t *tab, const Chains &ch, ChainWin &W, bool dense,
                                             const LaneSpan &L, uint32_t lane, uint32_t k0, bool has0,
-                                            uint64_t pred0, TeamState &B, uint64_t &rewalks, uint64_t &steps) {
+                                            uint64_t pred0, BlockState &B, uint64_t &rewalks, uint64_t &steps) {
     const bool mine = lane < kWalkSpans && L.act;
     uint64_t E = mine ? B.E[k0 + lane] : 0, X = mine ? B.X[k0 + lane] : 0;
     for (;;) {
@@ -1528,72 +1649,53 @@ __device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) {
     return __builtin_nontemporal_load((const g_u64 *)p);
 }
 
-// Phase timer (diag & 128): per-wave durations in registers, summed at the
-// worker's end.
+// Phase timer (diag & 128): per-wave durations in registers, summed per block
+// at the end (one atomic per phase per block, not per wave).
 #define CDC_DIAG_T(k)                                                  \
     do {                                                               \
         if (fp.diag & 128) {                                           \
             const uint64_t t_ = __builtin_amdgcn_s_memrealtime();       \
-            us.dt[k] += t_ - t_prev;                                   \
+            dt[k] += t_ - t_prev;                                      \
             t_prev = t_;                                               \
         }                                                              \
     } while (0)
-
-// Per-block LDS of the resolve waves: the GEAR table, each wave's window, the
-// team's span states, its barrier and its statistics.
-struct ResTeam {
-    uint64_t tab[256];
-    ChainWin win[kTeam];
-    TeamState ts;
-    unsigned long long stat[4];  // candidates << 24 | overflowed, re-walks, exact steps, errors
-    uint64_t unit;               // the unit the team claimed
-    uint32_t bar_cnt, bar_gen;
-};
-
-// Barrier of the kTeam resolve waves (the fused kernel's scan waves never
-// join it): an LDS arrival counter and a generation word.
-__device__ __forceinline__ void team_barrier(ResTeam &T, uint32_t lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) {
-        const uint32_t g = __hip_atomic_load(&T.bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (__hip_atomic_fetch_add(&T.bar_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == kTeam - 1) {
-            __hip_atomic_store(&T.bar_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&T.bar_gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-            while (__hip_atomic_load(&T.bar_gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == g)
-                __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 // FastParams.diag (CHUNKFS_AMD_DIAG, read at cdc_create) -- test hooks and
 // timing experiments only, 0 in every real run: 1 = walks start at the span
 // start (no warm-up: nearly every boundary re-walks), 2 = every wave takes the
 // dense (global record list) path, 128 = phase timings into the stats.
-// Wave tw of the team resolves spans k0 = tw * kWalkSpans .. of unit b.
-__device__ void resolve_unit(const ResArgs &a, const FastParams &fp, uint64_t b, ResTeam &T, uint32_t tw,
-                             uint32_t lane, UnitStats &us) {
-    const StreamTable &st = a.st;
-    const Candidates &cand = a.cand;
-    const Chains &ch = a.ch;
-    const Compact &cp = a.cp;
-    const Resolve &rs = a.rs;
-    ChainWin &W = T.win[tw];
-    TeamState &B = T.ts;
-    const uint64_t *tab = T.tab;
+__global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTable st, const FastParams fp,
+                                                              const uint64_t *__restrict__ gear,
+                                                              const Candidates cand, const Chains ch,
+                                                              const Compact cp, const Resolve rs,
+                                                              cdc_chunk_pod *out, uint64_t out_cap) {
+    __shared__ uint64_t tab[256];
+    __shared__ ChainWin win[kResWaves];
+    __shared__ BlockState B;
+    // Blocks take their index in dispatch order, so the look-back only ever
+    // waits on blocks that are already running or done.
+    if (threadIdx.x == 0) {
+        B.b = atomicAdd((unsigned long long *)&cp.stats[kStatOrder], 1ull);
+        B.base = B.pred = 0;
+        B.rewalk = 0;
+    }
+    load_tab1(tab, gear);
+    const uint64_t b = B.b;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t sl2 = st.span_log2;
     const uint64_t span = 1ull << sl2;
-    const uint64_t g0 = b * kTeamSpans;
-    const uint32_t nsp = (uint32_t)min((uint64_t)kTeamSpans, st.total_spans - g0);
-    const uint32_t k0 = tw * kWalkSpans;  // unit index of this wave's first span
+    const uint64_t g0 = b * kBlockSpans;
+    const uint32_t nsp = (uint32_t)min((uint64_t)kBlockSpans, st.total_spans - g0);
+    const uint32_t k0 = wave * kWalkSpans;  // block index of this wave's first span
     const uint64_t G0 = g0 + k0;
     const uint32_t cap = cand.cap;
+    ChainWin &W = win[wave];
     uint64_t t_prev = (fp.diag & 128) ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t dt[kStatDiagN] = {};
     uint64_t steps = 0, rewalks = 0, cstat = 0;
     LaneSpan L{};
     bool dense = false;
+
     if (k0 < nsp) {
         const int64_t gfirst = (int64_t)G0 - kWarmSpans;  // span of slot 0
         // 1. window metadata, then every record of the window (one batch of loads)
@@ -1693,11 +1795,11 @@ __device__ void resolve_unit(const ResArgs &a, const FastParams &fp, uint64_t b,
                 // one memory latency per round instead of one per pass)
                 LinkItem A = link_item(W, fp, virt, e0 + lane, e1);
                 uint32_t wa[13];
-                item_load(A, cand.pos, wa);
+                item_load(A, gear, wa);
                 for (uint32_t base = e0; base < e1; base += 64) {
                     const LinkItem B2 = link_item(W, fp, virt, base + 64 + lane, e1);
                     uint32_t wb[13];
-                    item_load(B2, cand.pos, wb);
+                    item_load(B2, gear, wb);
                     const uint32_t tr = (fp.diag & 4) ? kTruncNone : item_trunc(A, wa, fp, tab);
                     item_link(W, fp, tab, A, tr, sl2, nv);
                     A = B2;
@@ -1742,18 +1844,21 @@ __device__ void resolve_unit(const ResArgs &a, const FastParams &fp, uint64_t b,
         }
         CDC_DIAG_T(5);
     }
-    team_barrier(T, lane);
+    __syncthreads();
 
-    // 5-6. unit settle (round 0), then the look-back; a unit whose entry turns
-    // out stale settles again from the predecessor's final exit (round 1).
+    // 5-6. block settle (round 0), then the look-back; a block whose entry
+    // turns out stale settles again from the predecessor's final exit (round 1).
 #pragma unroll 1
     for (int round = 0; round < 2; ++round) {
         bool need;
-        if (round == 0) {  // (every wave reads the same LDS: a uniform answer)
-            need = __ballot(lane > 0 && lane < nsp && !B.F[lane] && B.E[lane] != B.X[lane - 1]) != 0;
+        if (round == 0) {
+            const uint32_t k = threadIdx.x;
+            need = __syncthreads_or(k > 0 && k < nsp && !B.F[k] && B.E[k] != B.X[k - 1]) != 0;
         } else {
-            if (tw == 0) {
-                const uint64_t C = wave_sum(lane < nsp ? (uint64_t)B.N[lane] : 0ull);
+            if (wave == 0) {
+                uint64_t C = 0;
+                for (uint32_t k = lane; k < nsp; k += 64) C += B.N[k];
+                C = wave_sum(C);
                 const uint64_t Eb = B.F[0] ? kNoDep : B.E[0];
                 const uint64_t Xb = B.X[nsp - 1];
                 uint64_t acc = 0, pred = 0;
@@ -1763,29 +1868,31 @@ __device__ void resolve_unit(const ResArgs &a, const FastParams &fp, uint64_t b,
                     ok = lookback(rs, b, Eb, lane, acc, pred);
                 }
                 if (ok != 0) publish(rs, b, kInc, acc + C, 0, Xb, lane);  // (a timeout too: never strand waiters)
-                if (ok < 0) ++us.err;
                 if (lane == 0) {
                     B.base = acc;
                     B.pred = pred;
                     B.rewalk = ok == 0 ? 1u : 0u;
+                    if (ok < 0) atomicAdd((unsigned long long *)&cp.stats[kStatError], 1ull);
                 }
                 CDC_DIAG_T(6);
             }
-            team_barrier(T, lane);
+            __syncthreads();
             need = B.rewalk != 0;
         }
         if (need) {
-            for (uint32_t w2 = 0; w2 < (uint32_t)kTeam; ++w2) {
-                if (tw == w2 && k0 < nsp)
+            for (uint32_t w2 = 0; w2 < (uint32_t)kResWaves; ++w2) {
+                if (wave == w2 && k0 < nsp)
                     wave_settle(st, fp, cand, tab, ch, W, dense, L, lane, k0, w2 > 0 || round > 0,
                                 w2 > 0 ? B.X[k0 - 1] : B.pred, B, rewalks, steps);
-                team_barrier(T, lane);
+                __syncthreads();
             }
         }
     }
     CDC_DIAG_T(2);
-    if (B.rewalk && tw == 0) {
-        const uint64_t C = wave_sum(lane < nsp ? (uint64_t)B.N[lane] : 0ull);
+    if (B.rewalk && wave == 0) {
+        uint64_t C = 0;
+        for (uint32_t k = lane; k < nsp; k += 64) C += B.N[k];
+        C = wave_sum(C);
         publish(rs, b, kInc, B.base + C, 0, B.X[nsp - 1], lane);
     }
 
@@ -1804,7 +1911,7 @@ __device__ void resolve_unit(const ResArgs &a, const FastParams &fp, uint64_t b,
         if (lane == 0) W.wpre[0] = 0;
         const uint32_t wtot = (uint32_t)__shfl(x, kWalkSpans - 1);
         const uint64_t obase = B.base + wpre0;
-        const bool bad = __ballot(L.act && myN > ch.smax) != 0 || obase + wtot > a.out_cap;
+        const bool bad = __ballot(L.act && myN > ch.smax) != 0 || obase + wtot > out_cap;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's chunk-start stores, before its loads
         wave_sync_lds();
         if (!bad) {
@@ -1817,250 +1924,78 @@ __device__ void resolve_unit(const ResArgs &a, const FastParams &fp, uint64_t b,
                 const uint64_t s0 = r < kLdsStarts ? off_k + W.st[k][r] : ld_nt(list + r);
                 const uint64_t nx = r + 1 >= B.N[k0 + k] ? B.X[k0 + k]
                                     : r + 1 < kLdsStarts ? off_k + W.st[k][r + 1] : ld_nt(list + r + 1);
-                a.out[obase + i] = cdc_chunk_pod{s0, nx - s0};
+                out[obase + i] = cdc_chunk_pod{s0, nx - s0};
             }
             if (L.act) {
                 if (L.first) cp.h_first[L.si] = obase + x - myN;
                 if (L.g + 1 == st.total_spans) cp.h_first[st.n] = obase + x;
             }
-        } else {
-            ++us.err;
         }
-        us.cand += wave_sum(cstat);
-        us.rewalk += wave_sum(rewalks);
-        us.steps += wave_sum(steps);
+        const uint64_t cs = wave_sum(cstat), rw = wave_sum(rewalks), sp = wave_sum(steps);
+        if (lane == 0) {
+            B.stat[wave][0] = cs;
+            B.stat[wave][1] = rw;
+            B.stat[wave][2] = sp + (bad ? (1ull << 40) : 0);
+        }
         CDC_DIAG_T(7);
+    } else if (lane == 0) {
+        B.stat[wave][0] = B.stat[wave][1] = B.stat[wave][2] = 0;
     }
-    team_barrier(T, lane);  // (the team's state is reused by its next unit)
+    if ((fp.diag & 128) && lane == 0)
+        for (int k = 0; k < kStatDiagN; ++k) B.diag[wave][k] = dt[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t cs = 0, rw = 0, sp = 0;
+        for (int w = 0; w < kResWaves; ++w) {
+            cs += B.stat[w][0];
+            rw += B.stat[w][1];
+            sp += B.stat[w][2];
+        }
+        if (fp.diag & 128)
+            for (int k = 0; k < kStatDiagN; ++k) {
+                uint64_t d = 0;
+                for (int w = 0; w < kResWaves; ++w) d += B.diag[w][k];
+                atomicAdd((unsigned long long *)&cp.stats[kStatDiag0 + k], (unsigned long long)d);
+            }
+        const uint64_t err = sp >> 40;
+        sp &= (1ull << 40) - 1;
+        if (cs) atomicAdd((unsigned long long *)&cp.stats[kStatCand], (unsigned long long)cs);
+        if (rw) atomicAdd((unsigned long long *)&cp.stats[kStatRewalk], (unsigned long long)rw);
+        if (sp) atomicAdd((unsigned long long *)&cp.stats[kStatOnDemand], (unsigned long long)sp);
+        if (err) atomicAdd((unsigned long long *)&cp.stats[kStatError], (unsigned long long)err);
+        __threadfence();
+        if (atomicAdd((unsigned long long *)&cp.stats[kStatTicket], 1ull) + 1 == gridDim.x) {
+            __threadfence();
+            for (int i = 0; i < kStatWords; ++i)
+                if (i != kStatDone) cp.h_stats[i] = ld_agent(&cp.stats[i]);
+            const uint64_t c = cp.h_stats[kStatCand];
+            cp.h_stats[kStatCand] = c >> 24;
+            cp.h_stats[kStatOvf] = c & 0xFFFFFF;
+            __threadfence_system();
+            cp.h_stats[kStatDone] = 1;
+        }
+    }
 }
 #undef CDC_DIAG_T
-
-// A team: units claimed in dispatch order (one counter per batch, so a
-// look-back only ever waits on units that running teams hold -- teams of other
-// launches or processes sharing the device may keep some of ours waiting for
-// a CU, never deadlocked), then its statistics into its slot of a.part and a
-// ticket; the batch's last team sums every slot into the host-coherent stats
-// and sets the done word.
-__device__ void resolve_worker(const ResArgs &a, const FastParams &fp, ResTeam &T, uint32_t tw, uint32_t lane,
-                               uint64_t t, uint64_t nt) {
-    if (a.units == 0) return;  // (a fused scan with no batch to resolve)
-    UnitStats us;
-    for (;;) {
-        if (tw == 0 && lane == 0) T.unit = atomicAdd((unsigned long long *)&a.cp.stats[kStatOrder], 1ull);
-        team_barrier(T, lane);
-        const uint64_t u = T.unit;  // (rewritten only after the unit's last team barrier)
-        if (u >= a.units) break;
-        resolve_unit(a, fp, u, T, tw, lane, us);
-    }
-    if (lane == 0) {
-        atomicAdd(&T.stat[0], (unsigned long long)us.cand);
-        atomicAdd(&T.stat[1], (unsigned long long)us.rewalk);
-        atomicAdd(&T.stat[2], (unsigned long long)us.steps);
-        atomicAdd(&T.stat[3], (unsigned long long)us.err);
-        if (fp.diag & 128)
-            for (int k = 0; k < kStatDiagN; ++k)
-                atomicAdd((unsigned long long *)&a.cp.stats[kStatDiag0 + k], (unsigned long long)us.dt[k]);
-    }
-    team_barrier(T, lane);
-    if (tw != 0 || lane != 0) return;
-    uint64_t *part = a.part + t * 4;
-    for (int k = 0; k < 4; ++k)
-        st_agent(&part[k], __hip_atomic_load(&T.stat[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    __threadfence();
-    if (atomicAdd((unsigned long long *)&a.cp.stats[kStatTicket], 1ull) + 1 != nt) return;
-    __threadfence();
-    uint64_t tot[4] = {0, 0, 0, 0};
-    for (uint64_t blk = 0; blk < nt; ++blk)
-        for (int k = 0; k < 4; ++k) tot[k] += ld_agent(a.part + blk * 4 + k);
-    for (int i = 0; i < kStatWords; ++i)
-        if (i != kStatDone) a.cp.h_stats[i] = ld_agent(&a.cp.stats[i]);
-    a.cp.h_stats[kStatCand] = tot[0] >> 24;
-    a.cp.h_stats[kStatOvf] = tot[0] & 0xFFFFFF;
-    a.cp.h_stats[kStatRewalk] = tot[1];
-    a.cp.h_stats[kStatOnDemand] = tot[2];
-    a.cp.h_stats[kStatError] = tot[3];
-    __threadfence_system();
-    a.cp.h_stats[kStatDone] = 1;
-}
-
-__device__ __forceinline__ void res_team_init(ResTeam &T, const uint64_t *gear, uint32_t tid, uint32_t nthreads) {
-    for (uint32_t i = tid; i < 256; i += nthreads) T.tab[i] = gear[i];
-    if (tid < 4) T.stat[tid] = 0;
-    if (tid == 0) T.bar_cnt = T.bar_gen = 0;
-}
-
-#ifndef CDC_RES_MINW
-#define CDC_RES_MINW 2  // waves per SIMD the standalone resolve is compiled for (VGPR budget)
-#endif
-// Standalone resolve: one team per block.
-__global__ __launch_bounds__(kResThreads, CDC_RES_MINW) void resolve_kernel(const ResArgs a, const FastParams fp,
-                                                                          const uint64_t *__restrict__ gear) {
-    __shared__ ResTeam T;
-    res_team_init(T, gear, threadIdx.x, kResThreads);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t tw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    resolve_worker(a, fp, T, tw, lane, blockIdx.x, gridDim.x);
-}
-
-// ---- scan kernel (after the resolve: the fused launch runs resolve workers) ----
-
-// Full spans.  Lane l owns the contiguous segment [l*sub, (l+1)*sub) and
-// hashes it serially from hash 0; its first 48 positions are re-tested at the
-// end with the true carry-in (lane l-1's final hash, one DPP shift; lane 0's
-// from the 48 bytes before the span).  Ragged last spans: scan_tail_kernel.
-//
-// kRes (the fused launch): kTeam more waves per block resolve the PREVIOUS
-// batch of the handle (`ra`, its own double-buffered candidates and stats)
-// while the kW scan waves scan this one -- one wave per SIMD beside three
-// scanning ones (12 scan waves per CU scan as fast as 16,
-// profiles/r05/r05v_scan_12_waves.log), in the LDS the 12-wave scan leaves.
-template <bool kAlign, int kW, int kLook, int kMode, bool kRes>
-__global__ __launch_bounds__((kW + (kRes ? kTeam : 0)) * 64, 1) void scan_kernel(
-    const StreamTable st, const FastParams fp, const uint64_t *__restrict__ gear, const Candidates cand,
-    const Compact cp, const ResArgs ra) {
-    constexpr int kThreads = (kW + (kRes ? kTeam : 0)) * 64;
-    __shared__ ScanLds<kW> L;
-    __shared__ typename std::conditional<kRes, ResTeam, char>::type RT;
-    const uint64_t *tab = L.tab;
-    for (int i = threadIdx.x; i < 256 * kCopies; i += kThreads)
-        L.tab[i] = gear[i / kCopies] << fp.tshift;  // pre-shifted GEAR (see FastParams)
-    if constexpr (kRes) res_team_init(RT, gear, threadIdx.x, kThreads);
-    if (blockIdx.x == 0 && threadIdx.x < kStatWords) cp.stats[threadIdx.x] = 0;  // the resolve accumulates
-    __syncthreads();
-
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
-    if constexpr (kRes) {
-        const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave);
-        if (wv >= (uint32_t)kW) {
-            resolve_worker(ra, fp, RT, wv - kW, lane, blockIdx.x, gridDim.x);
-            return;
-        }
-    }
-    const uint32_t rep = (lane & 31) * 8;  // this lane's GEAR replica
-    const uint64_t span = 1ull << st.span_log2;
-    const uint32_t sub_log2 = st.span_log2 - 6;
-    const uint32_t sub = 1u << sub_log2;   // bytes per lane per span (>= 1 KiB)
-    const uint32_t steps = sub / kStep;    // >= 16, a power of two
-    const uint32_t lo = lane << sub_log2;  // lane's first byte in the span
-    const uint64_t istride = 16ull * sub;
-    const EntryList E{L.epos[wave], L.ehlo[wave], L.ehhi[wave], L.ecnt[wave]};
-    // Instruction i's lane quad u = lane/4 loads row 16 i + rsel(u); the two
-    // quads of one ds_write_b128 lane group (8 lanes) get rows 4 apart, so
-    // their 80-byte rows sit 16 banks apart and the write is conflict-free
-    // (rows u, u+1 collided on one 4-bank group: 8 extra LDS cycles per
-    // store, r02av PMC); the reads (lane = row) are unchanged.
-    const uint32_t rsel = ((lane >> 3) & 3) + 8 * (lane >> 5) + 4 * ((lane >> 2) & 1);
-    uint4 *wrow = &L.stage[wave][rsel * 5 + (lane & 3)];
-    const uint4 *rrow = &L.stage[wave][lane * 5];
-
-    // Spans are software-pipelined: the first two steps of the next span are
-    // in flight while this span's fix-up and flush run.  Ragged last spans:
-    // scan_tail_kernel.
-    const uint64_t gstride = (uint64_t)gridDim.x * kW;
-    auto next_full = [&](uint64_t g, uint32_t &si, uint64_t &off) {
-        for (; g < st.total_spans; g += gstride) {
-            locate(st, g, si, off);
-            if (st.lens[si] - off >= span) break;
-        }
-        return g;
-    };
-    Q4 A, B, C;
-    uint32_t si, wb = 0;
-    uint64_t off;
-    uint64_t g = next_full((uint64_t)blockIdx.x * kW + wave, si, off);
-    const uint8_t *base = nullptr, *gp = nullptr;
-    auto prefetch = [&]() {  // first two steps and the carry bytes of span g
-        base = st.ptrs[si] + off;
-        gp = base + (uint64_t)rsel * sub + (lane & 3) * 16;
-        wb = 0;
-        if (off != 0 && lane < 48) wb = as_global1(base)[(int)lane - 48];
-        gload_step(A, gp, istride, 0);
-        SCHED_FENCE();
-        gload_step(B, gp, istride, 1);
-        SCHED_FENCE();
-    };
-    if (g < st.total_spans) prefetch();
-    while (g < st.total_spans) {
-        uint32_t ne = 0;  // quarter entries appended this span (wave-uniform)
-        uint64_t h = 0;
-        uint4 F0, F1, F2;
-        // Two steps in flight while one is hashed (A/B ring).  The loop body
-        // issues its loads unconditionally -- a conditional load leaves the
-        // compiler unsure how many are outstanding at the back edge, and it
-        // then waits for all of them -- so the last two steps are peeled.
-        stage_step(C, A, wrow, rrow);
-        F0 = C.q[0];
-        F1 = C.q[1];
-        F2 = C.q[2];
-        gload_step(A, gp, istride, 2);
-        SCHED_FENCE();
-// kMode: 0 = the scan; 1 = loads and transposes only, 2 = hashing only (timing
-// experiments: CHUNKFS_AMD_DIAG bits 8-9, results meaningless).
-#define CDC_PROC(POS)                                                                          \
-    do {                                                                                       \
-        if constexpr (kMode == 1) h ^= (uint64_t)(C.q[0].x ^ C.q[1].y ^ C.q[2].z ^ C.q[3].w);   \
-        else process_step<kAlign, kLook>(C, h, POS, ne, E, tab, rep, fp);                      \
-    } while (0)
-#define CDC_SCAN_PAIR(T, LOAD_B, STAGE_A, LOAD_A)                                              \
-    do {                                                                                       \
-        CDC_PROC(lo + (T) * kStep);                                                            \
-        SCHED_FENCE();                                                                         \
-        stage_step(C, B, wrow, rrow);                                                          \
-        if (LOAD_B && kMode != 2) gload_step(B, gp, istride, (T) + 3);                         \
-        SCHED_FENCE();                                                                         \
-        CDC_PROC(lo + ((T) + 1) * kStep);                                                      \
-        SCHED_FENCE();                                                                         \
-        if (STAGE_A) stage_step(C, A, wrow, rrow);                                             \
-        if (LOAD_A && kMode != 2) gload_step(A, gp, istride, (T) + 4);                         \
-        SCHED_FENCE();                                                                         \
-    } while (0)
-        uint32_t t = 0;
-        for (; t + 4 < steps; t += 2) CDC_SCAN_PAIR(t, true, true, true);
-        CDC_SCAN_PAIR(t, true, true, false);        // steps-4, steps-3
-        CDC_SCAN_PAIR(t + 2, false, false, false);  // steps-2, steps-1
-#undef CDC_SCAN_PAIR
-#undef CDC_PROC
-        // This span's carry-in bytes and identity, then the next span's prefetch.
-        const uint64_t g_cur = g, off_cur = off;
-        const uint64_t avail_cur = st.lens[si] - off;
-        const uint32_t wb_cur = wb;
-        const uint8_t *base_cur = base;
-        g = next_full(g + gstride, si, off);
-        if (g < st.total_spans) prefetch();
-        // Fix-up: re-test the first 48 positions with the true carry-in.
-        const uint64_t gw = lane < 48 ? L.tab[wb_cur * kCopies + (lane & 31)] : 0;
-        const uint64_t hw = readlane_u64(gear_prefix(gw, lane), 47);  // hash of the 48 bytes before
-        h = wave_shr1(h, off_cur != 0 ? hw : 0);
-        {
-            uint64_t h0 = h;
-            append_hits(quarter<kAlign>(h, F0, tab, rep, fp) == 0, lo | kEntFix, h0, ne, E);
-            h0 = h;
-            append_hits(quarter<kAlign>(h, F1, tab, rep, fp) == 0, (lo + 16) | kEntFix, h0, ne, E);
-            h0 = h;
-            append_hits(quarter<kAlign>(h, F2, tab, rep, fp) == 0, (lo + 32) | kEntFix, h0, ne, E);
-        }
-        flush_span(g_cur, base_cur, (uint32_t)span, avail_cur, sub - 1, ne, E, tab, rep, fp, cand, lane);
-    }
-}
 
 }  // namespace
 
 hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
                        const Candidates &cand, const Compact &cp, const uint64_t *d_tails, uint32_t n_tails,
-                       int num_cus, const ResArgs &prev, hipStream_t s) {
+                       int num_cus, hipStream_t s) {
+    if (!st.total_spans) return hipSuccess;
     if (n_tails) {
         if (fp.cm_align)
             scan_tail_kernel<true><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, d_tails);
         else
             scan_tail_kernel<false><<<n_tails, 64, 0, s>>>(st, fp, d_gear, cand, d_tails);
     }
-    // 12 scan waves per CU (as fast as 16) + 4 resolve waves for the previous
-    // batch; GEAR lookups one dword ahead of the chain.
+    // 12 waves per CU (3 per SIMD: as fast as 16, r05v_scan_12_waves.log, with
+    // up to 168 VGPRs), GEAR lookups one dword ahead of the chain.  (Measured:
+    // 12 waves with two dwords of lookahead is slower.)
     constexpr int W = CDC_SCAN_WAVES, K = CDC_SCAN_LOOK;
     const uint32_t mode = (fp.diag >> 8) & 3;
-    if (st.total_spans && mode == 0 && (fp.diag & kDiagDmaScan) && prev.units == 0) {  // LDS-DMA landing (A/B)
+    if (mode == 0 && (fp.diag & kDiagDmaScan)) {  // LDS-DMA input landing (measured, not adopted)
         const uint64_t groups = (st.total_spans + kDmaW - 1) / kDmaW;
         const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
         if (fp.cm_align)
@@ -2069,34 +2004,29 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
             scan_dma_kernel<false><<<grid, kDmaW * 64, 0, s>>>(st, fp, d_gear, cand, cp);
         return hipGetLastError();
     }
-    if (!st.total_spans && prev.units == 0) return hipSuccess;
-    // every CU when a previous batch is resolved beside the scan (a team per block)
-    const uint64_t groups = prev.units ? (uint64_t)num_cus : (st.total_spans + W - 1) / W;
+    const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
-    constexpr int T = (W + kTeam) * 64;
     if (mode == 1 && fp.cm_align)
-        scan_kernel<true, W, K, 1, true><<<grid, T, 0, s>>>(st, fp, d_gear, cand, cp, prev);
+        scan_kernel<true, W, K, 1><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else if (mode == 2 && fp.cm_align)
-        scan_kernel<true, W, K, 2, true><<<grid, T, 0, s>>>(st, fp, d_gear, cand, cp, prev);
+        scan_kernel<true, W, K, 2><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else if (fp.cm_align)
-        scan_kernel<true, W, K, 0, true><<<grid, T, 0, s>>>(st, fp, d_gear, cand, cp, prev);
+        scan_kernel<true, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     else
-        scan_kernel<false, W, K, 0, true><<<grid, T, 0, s>>>(st, fp, d_gear, cand, cp, prev);
+        scan_kernel<false, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
     return hipGetLastError();
 }
 
-uint64_t resolve_units(uint64_t spans) { return (spans + kTeamSpans - 1) / kTeamSpans; }
+uint64_t resolve_blocks(uint64_t spans) { return (spans + kBlockSpans - 1) / kBlockSpans; }
 
-hipError_t launch_resolve(const ResArgs &a, const FastParams &fp, const uint64_t *d_gear, int num_cus,
-                          hipStream_t s) {
-    if (!a.units) return hipSuccess;
-    // up to CDC_RES_MINW teams per CU, each claiming units until none is left
-    const uint64_t want = a.units, cap = (uint64_t)num_cus * CDC_RES_MINW;
-    resolve_kernel<<<(unsigned)(want < cap ? want : cap), kResThreads, 0, s>>>(a, fp, d_gear);
+hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
+                          const Candidates &cand, const Chains &ch, const Compact &cp, const Resolve &rs,
+                          void *d_out, uint64_t out_cap, hipStream_t s) {
+    if (!st.total_spans) return hipSuccess;
+    resolve_kernel<<<(unsigned)resolve_blocks(st.total_spans), kResThreads, 0, s>>>(
+        st, fp, d_gear, cand, ch, cp, rs, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap);
     return hipGetLastError();
 }
-
-uint32_t resolve_part_words(int num_cus) { return (uint32_t)num_cus * CDC_RES_MINW * 4 + 64; }
 
 }  // namespace p3
 }  // namespace cdc

@@ -2108,6 +2108,14 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
 #ifndef CDC_RABIN_WAVES
 #define CDC_RABIN_WAVES 8
 #endif
+// Skewed replicas (CDC_RABIN_SKEW=1): entry e's 16 replicas at e * 136 bytes
+// (17 slots), so the bank of a lookup depends on the entry too -- lanes l and
+// l+16 share a replica and used to collide on every lookup (bank = 2r only:
+// 48 % of LDS cycles were conflicts, profiles/r04_walk/r04f_pmc_walk.txt);
+// with the skew they collide when their entries agree mod 16.
+#ifndef CDC_RABIN_SKEW
+#define CDC_RABIN_SKEW 0  // measured slower: 1262 vs 1346 GiB/s (profiles/r05/r05g_rabin_*.log)
+#endif
 constexpr int kRabinReps = CDC_RABIN_REPS;
 constexpr int kRabinWaves = CDC_RABIN_WAVES;  // pieces per block (64 KiB of tables shared by 8 waves)
 
@@ -2120,17 +2128,31 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     // (out: the leaving byte) or one v_lshl_or (mod: the digest's top byte).
     // (Two interleaved chains per lane -- more independent lookups in flight
     // -- need ~2x the registers and spilled at the 128 VGPRs of 16 waves / CU.)
+#if CDC_RABIN_SKEW
+    constexpr uint32_t kStride = 136;  // bytes per entry (17 slots of 8: 16 replicas + a skew slot)
+    __shared__ uint64_t rt[2 * 256 * 17];  // mod table, then out table
+    static_assert(kRabinReps == 16, "rbits_kernel: 16 replicas per table");
+    for (int i = threadIdx.x; i < 2 * 256 * 17; i += 64 * kRabinWaves) {
+        const int t = i / (256 * 17), e = (i % (256 * 17)) / 17;
+        rt[i] = wp.tabs[(t ? 256 : 0) + e];
+    }
+#else
     __shared__ uint64_t rt[256 * 32];
     static_assert(kRabinReps == 16, "rbits_kernel: 16 replicas per table");
     for (int i = threadIdx.x; i < 256 * 32; i += 64 * kRabinWaves) {
         const int e = i >> 5, k = i & 31;
         rt[i] = wp.tabs[(k < 16 ? 0 : 256) + e];
     }
+#endif
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
     if (!piece_of(st, wp, (uint64_t)blockIdx.x * kRabinWaves + wave_id(), pc)) return;
+#if CDC_RABIN_SKEW
+    const uint32_t om = (lane & 15) * 8, oo = 256 * kStride + om;  // this lane's mod / out replica
+#else
     const uint32_t om = (lane & 15) * 8, oo = 128 + om;  // this lane's mod / out replica
+#endif
     lds_wchar *tb = (lds_wchar *)rt;
     const uint64_t len = st.lens[pc.si];
     const uint8_t *base = st.ptrs[pc.si];
@@ -2146,11 +2168,19 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const uint32_t ow = word_of(old, j >> 2), cw = word_of(cur, j >> 2);
+#if CDC_RABIN_SKEW
+                const uint32_t ao = __umul24((ow >> (8 * (j & 3))) & 0xFFu, kStride) + oo;
+#else
                 const uint32_t ao = __builtin_amdgcn_perm(oo, ow, 0x0c0c0004u | ((uint32_t)(j & 3) << 8));
+#endif
                 const uint64_t o = *reinterpret_cast<lds_w64 *>(tb + ao);
                 lo ^= (uint32_t)o;
                 hi ^= (uint32_t)(o >> 32);
+#if CDC_RABIN_SKEW
+                const uint64_t m = *reinterpret_cast<lds_w64 *>(tb + (__umul24(hi >> tsh, kStride) + om));
+#else
                 const uint64_t m = *reinterpret_cast<lds_w64 *>(tb + (((hi >> tsh) << 8) | om));
+#endif
                 hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
                 // (lo << 8) | the entering byte, one v_perm
                 lo = __builtin_amdgcn_perm(lo, cw, 0x06050400u | (uint32_t)(j & 3)) ^ (uint32_t)m;

@@ -146,10 +146,10 @@ int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
 
 /* The same batch, enqueued: returns 0 once the batch is submitted, and
  * `first` (kept by the library until then) is filled by cdc_batch_sync.
- * FastCDC batches of more than 8 MiB are pipelined on the device: the scan
- * launch of batch k also resolves batch k-1 (the resolve waves run beside the
- * scan waves), so back-to-back batches pay the resolve off the critical
- * path; d_streams' bytes and d_out must stay untouched until cdc_batch_sync.
+ * FastCDC batches of more than 8 MiB are enqueued back to back on the stream
+ * (scan, resolve, next scan ...) with no host round trip between them, their
+ * results collected later; d_streams' bytes and d_out must stay untouched
+ * until cdc_batch_sync.
  * Consecutive async batches of one handle must use one hip_stream (another
  * stream first completes the batches in flight).  Smaller FastCDC batches
  * and other algorithms complete inside this call (first filled on return).

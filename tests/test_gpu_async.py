@@ -1,9 +1,9 @@
-"""Pipelined FastCDC batches (cdc_chunk_batch_device_async / cdc_batch_sync).
+"""Asynchronous FastCDC batches (cdc_chunk_batch_device_async / cdc_batch_sync).
 
-The scan launch of batch k also resolves batch k-1 (fused resolve waves), so
-every batch of a burst but the last is resolved beside the next one's scan,
-from its own double-buffered candidates and statistics.  Every batch's chunks
-must equal the oracle's, whatever the interleaving: multi-stream batches,
+Batches of more than 8 MiB are enqueued back to back with no host wait, each
+with its own host staging block (three in rotation) and device table slot
+(two); results are collected later.  Every batch's chunks must equal the
+oracle's, whatever the interleaving: multi-stream batches,
 ragged and empty streams, different outputs per batch, bursts ended by
 cdc_batch_sync or by a synchronous call, and small batches that complete
 inside the call.  Parity vs the fastcdc crate is unpinned (GEAR placeholder,
