@@ -40,29 +40,37 @@ __global__ void fill_kernel(uint8_t *buf, uint64_t len, uint64_t seed) {
 }
 
 // Read-only reduction (the measured-achievable HBM read rate the FastCDC scan
-// is compared with): every byte read once with 16-byte
-// coalesced loads, four in flight per lane, XOR-folded; one word per block.
-__global__ __launch_bounds__(256) void read_kernel(const uint4 *__restrict__ p, uint64_t n16, uint64_t *out) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint32_t acc = 0;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+// is compared with): each block reads 16 KiB contiguous per
+// iteration, four 1 KiB-per-wave-instruction loads in flight per lane, XOR-
+// folded -- the fastest read pattern of tools/ubench_scan.hip (coalesced, 4 in
+// flight, 8 blocks per CU: 170 us per GiB, profiles/r02_ubench_scan.txt).
+typedef unsigned int rd_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void read_kernel(const uint8_t *d, uint64_t n, uint64_t *out) {
+    constexpr uint64_t kPer = 256ull * 16 * 4;
+    rd_u32x4 acc = {0, 0, 0, 0};
+    const uint64_t full = n / kPer * kPer;
+    for (uint64_t b = (uint64_t)blockIdx.x * kPer; b < full; b += (uint64_t)gridDim.x * kPer) {
+        rd_u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            v[k] = *reinterpret_cast<const __attribute__((address_space(1))) rd_u32x4 *>(
+                d + b + ((uint64_t)k * 256 + threadIdx.x) * 16);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc ^= v[k];
     }
-    for (; i < n16; i += stride) {
-        const uint4 a = p[i];
-        acc ^= a.x ^ a.y ^ a.z ^ a.w;
-    }
-    for (int o = 32; o > 0; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, o);
-    if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned int *>(out + blockIdx.x), acc);
+    for (uint64_t i = full + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; i + 16 <= n;
+         i += (uint64_t)gridDim.x * 256 * 16)
+        acc ^= *reinterpret_cast<const __attribute__((address_space(1))) rd_u32x4 *>(d + i);
+    uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    for (int o = 32; o > 0; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o);
+    if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned int *>(out + blockIdx.x), x);
 }
 
 }  // namespace
 
 hipError_t launch_read_reduce(const uint8_t *d_buf, uint64_t len, uint64_t *d_out, int num_cus, hipStream_t s) {
     if (len < 16) return hipSuccess;
-    read_kernel<<<(unsigned)(num_cus * 8), 256, 0, s>>>(reinterpret_cast<const uint4 *>(d_buf), len / 16, d_out);
+    read_kernel<<<(unsigned)(num_cus * 8), 256, 0, s>>>(d_buf, len, d_out);
     return hipGetLastError();
 }
 
