@@ -45,6 +45,7 @@ __global__ void fill_kernel(uint8_t *buf, uint64_t len, uint64_t seed) {
 // folded -- the fastest read pattern of tools/ubench_scan.hip (coalesced, 4 in
 // flight, 8 blocks per CU: 170 us per GiB, profiles/r02_ubench_scan.txt).
 typedef unsigned int rd_u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) rd_u32x4 g_rd_u32x4;
 __global__ __launch_bounds__(256) void read_kernel(const uint8_t *d, uint64_t n, uint64_t *out) {
     constexpr uint64_t kPer = 256ull * 16 * 4;
     rd_u32x4 acc = {0, 0, 0, 0};
@@ -53,14 +54,13 @@ __global__ __launch_bounds__(256) void read_kernel(const uint8_t *d, uint64_t n,
         rd_u32x4 v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            v[k] = *reinterpret_cast<const __attribute__((address_space(1))) rd_u32x4 *>(
-                d + b + ((uint64_t)k * 256 + threadIdx.x) * 16);
+            v[k] = *(g_rd_u32x4 *)(d + b + ((uint64_t)k * 256 + threadIdx.x) * 16);
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc ^= v[k];
     }
     for (uint64_t i = full + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; i + 16 <= n;
          i += (uint64_t)gridDim.x * 256 * 16)
-        acc ^= *reinterpret_cast<const __attribute__((address_space(1))) rd_u32x4 *>(d + i);
+        acc ^= *(g_rd_u32x4 *)(d + i);
     uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
     for (int o = 32; o > 0; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o);
     if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned int *>(out + blockIdx.x), x);
