@@ -989,6 +989,9 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 #define CDC_WIN_RECS 768
 #endif
 constexpr int kResWaves = CDC_RES_WAVES;
+#ifndef CDC_RES_FASTTRUNC
+#define CDC_RES_FASTTRUNC 1  // item_trunc's steady-regime test (A/B: 0)
+#endif
 constexpr int kResThreads = kResWaves * 64;
 
 // First hitting offset d in [0, tl-a0) of the truncated positions of the
@@ -1443,12 +1446,38 @@ __device__ __forceinline__ void item_load(const LinkItem &it, const void *safe, 
 // batch instead of one per 4 bytes), hit bits collected in a mask, the first
 // one wins (the same result as trunc_words).
 __device__ __forceinline__ uint32_t item_trunc(const LinkItem &it, const uint32_t (&w)[13], const FastParams &fp,
-                                               const uint64_t *tab) {
+                                               const uint64_t *tab, const uint64_t *tabs) {
     if (!it.act || it.len == 0) return kTruncNone;
     if (it.known != kTruncUnknown) return it.known;  // from the scan's flush
     if (!it.fast) return trunc_call(it.data, it.n, it.c, fp, tab);
     const uint32_t r = (uint32_t)(it.w0 & 3);
     const uint32_t ns = it.ce > it.a0 ? (uint32_t)min(it.ce - it.a0, (uint64_t)64) : 0u;  // d < ns: mask_s
+    if (CDC_RES_FASTTRUNC && fp.cm_align && it.len == kTruncMax && ns >= kTruncMax) {
+        // Steady regime (every tested position under mask_s): with the GEAR
+        // table pre-shifted by tshift the mask is the hash's high dword, so a
+        // position costs the chain step, one AND and one MIN; only a region
+        // that hits (~0.3 % of records) takes the exact loop below.
+        const uint32_t ms = (uint32_t)(fp.mask_s_sh >> 32);
+        uint64_t h = 0;
+        uint32_t acc = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k0 = 0; k0 < 12; k0 += 3) {
+            uint64_t g[12];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t a = __builtin_amdgcn_alignbyte(w[k0 + k + 1], w[k0 + k], r);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) g[4 * k + b] = tabs[(a >> (8 * b)) & 255];
+            }
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                if (4 * k0 + i >= (int)kTruncMax) break;
+                h = shl1_add(h, g[i]);
+                acc = min(acc, (uint32_t)(h >> 32) & ms);
+            }
+        }
+        if (acc != 0) return kTruncNone;
+    }
     uint64_t h = 0, hits = 0;
 #pragma unroll
     for (int k0 = 0; k0 < 12; k0 += 3) {
@@ -1670,6 +1699,7 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
                                                               const Compact cp, const Resolve rs,
                                                               cdc_chunk_pod *out, uint64_t out_cap) {
     __shared__ uint64_t tab[256];
+    __shared__ uint64_t tabs[256];  // the same, pre-shifted by tshift (item_trunc's steady-regime test)
     __shared__ ChainWin win[kResWaves];
     __shared__ BlockState B;
     // Blocks take their index in dispatch order, so the look-back only ever
@@ -1679,6 +1709,7 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
         B.base = B.pred = 0;
         B.rewalk = 0;
     }
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) tabs[i] = gear[i] << fp.tshift;
     load_tab1(tab, gear);
     const uint64_t b = B.b;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1800,7 +1831,7 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
                     const LinkItem B2 = link_item(W, fp, virt, base + 64 + lane, e1);
                     uint32_t wb[13];
                     item_load(B2, gear, wb);
-                    const uint32_t tr = (fp.diag & 4) ? kTruncNone : item_trunc(A, wa, fp, tab);
+                    const uint32_t tr = (fp.diag & 4) ? kTruncNone : item_trunc(A, wa, fp, tab, tabs);
                     item_link(W, fp, tab, A, tr, sl2, nv);
                     A = B2;
 #pragma unroll
