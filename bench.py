@@ -85,8 +85,8 @@ def parse(argv=None):
     p.add_argument("--config5-streams", type=int, default=16,
                    help="config 5: total streams, split across ranks (strong scaling)")
     p.add_argument("--config5-stream-bytes", type=int, default=1 << 30, help="config 5: bytes per stream")
-    p.add_argument("--config5-check", type=int, default=64 << 20,
-                   help="config 5: bytes of rank 0's first stream checked against the oracle")
+    p.add_argument("--config5-check", type=int, default=-1,
+                   help="config 5: bytes of the checked streams compared with the oracle (-1: whole streams)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)  # CPU launcher test only
     # Multi-rank rehearsal on a box with fewer GPUs than ranks (tests only):
@@ -297,10 +297,11 @@ def config5_leg(args, eng, rank, world, red_dev):
     SeqCDC) at avg 2 / 8 / 64 KiB, min = avg/4, max = 8 avg.
     Per (rule, sizes): one warm-up pass, then one pass bracketed by a barrier
     and a device sync on both sides; value = 16 GiB / max-over-ranks time.
-    Rank 0 checks the chunks of its first stream that lie in the first
-    --config5-check bytes against the oracle (all but the oracle's last chunk
-    there: these rules look only forward, so a prefix's chunks but its last
-    are the stream's).  SuperCDC is not implemented (CDC_ENOTSUP)."""
+    After the timed pass, rank 0's first stream -- and at N > 1 also the
+    first stream of the last rank -- is checked against the oracle, whole
+    (or its first --config5-check bytes: all chunks but the oracle's last
+    there, since these rules look only forward), the verdict a min over
+    ranks.  SuperCDC is not implemented (CDC_ENOTSUP)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -318,10 +319,12 @@ def config5_leg(args, eng, rank, world, red_dev):
     ptrs, lens = [b.data_ptr() for b in bufs], list(shard.lens)
     total = sharding.sum_over_ranks(sum(lens), red_dev)
     oracle = None
-    if rank == 0 and not args.no_parity and lens:
+    checker = rank == 0 or rank == world - 1  # rank 0 and, at N > 1, the last rank
+    whole = args.config5_check < 0 or (lens and args.config5_check >= lens[0])
+    if checker and not args.no_parity and lens:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        host0 = bufs[0][:min(args.config5_check, lens[0])].cpu().numpy()
+        host0 = bufs[0][:lens[0] if whole else args.config5_check].cpu().numpy()
     res = {}
     for avg in (2048, 8192, 65536):
         sz = cfa.SizeParams(avg // 4, avg, avg * 8)
@@ -345,10 +348,19 @@ def config5_leg(args, eng, rank, world, red_dev):
             line = {"sizes": [sz.min, sz.avg, sz.max], "GiBps": total / el / (1 << 30),
                     "frac_of_hbm": total / el / 1e9 / HBM_PEAK_GBS / world,
                     "chunks_total": sharding.sum_over_ranks(int(first[-1]), red_dev)}
+            ok = 1
             if oracle is not None:
-                ref = oracle.cdc(name, host0, sz.min, sz.avg, sz.max)[:-1]
-                got = out[:len(ref)].cpu().numpy().view(np.uint64) if len(ref) else np.zeros((0, 2), np.uint64)
-                line["parity_vs_oracle"] = bool(got.shape == ref.shape and (got == ref).all())
+                ref = oracle.cdc(name, host0, sz.min, sz.avg, sz.max)
+                if not whole:
+                    ref = ref[:-1]
+                    got = out[:len(ref)].cpu().numpy().view(np.uint64) if len(ref) else np.zeros((0, 2), np.uint64)
+                else:
+                    got = out[int(first[0]):int(first[1])].cpu().numpy().view(np.uint64)
+                ok = int(got.shape == ref.shape and bool((got == ref).all()))
+            if not args.no_parity and lens:
+                if world > 1:
+                    ok = sharding.min_over_ranks(ok, red_dev)
+                line["parity_vs_oracle"] = bool(ok)
             res[f"{name}_avg{avg // 1024}k"] = line
             ch.close()
             del out
@@ -357,8 +369,12 @@ def config5_leg(args, eng, rank, world, red_dev):
             "scaling": "strong",
             "streams_per_gpu": len(lens), "bytes_per_gpu": sum(lens),
             "frac_definition": "per-GPU bytes / max-over-ranks time / 8 TB/s",
-            "parity_definition": f"rank 0, stream 0, the chunks inside its first {args.config5_check} B" if oracle
-            is not None else None, "lines": res}
+            "parity_definition": (None if args.no_parity else
+                                  ("the whole first stream of rank 0" + (f" and of rank {world - 1}" if world > 1 else "")
+                                   + f" ({lens[0] if lens else 0} B each)") if whole else
+                                  f"rank 0 (and rank {world - 1}), stream 0, the chunks inside its first "
+                                  f"{args.config5_check} B"),
+            "lines": res}
 
 
 # ---------------------------------------------------------------------------
@@ -720,8 +736,41 @@ def host_path_leg(eng, w):
     import chunkfs_amd as cfa
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    hb = w.bufs[0][:w.lens[0]].cpu().numpy()
     ch = eng.ch
+    numa = cfa.host_placement(ch)
+    # The caller's thread joins the copy: run it (and place the source buffer)
+    # on the GPU's node too, as a NUMA-aware application would
+    # (CHUNKFS_AMD_COPY_NUMA=0: leave both where they are, A/B).
+    old_aff = os.sched_getaffinity(0)
+    if numa.get("numa_placement"):
+        try:
+            with open(f"/sys/devices/system/node/node{numa['gpu_node']}/cpulist") as f:
+                near = set(_parse_cpulist(f.read())) & old_aff
+            if near:
+                os.sched_setaffinity(0, near)
+                numa["caller_pinned_cpus"] = len(near)
+        except OSError:
+            pass
+    try:
+        return _host_path_leg(eng, w, ch, numa)
+    finally:
+        os.sched_setaffinity(0, old_aff)
+
+
+def _parse_cpulist(s):
+    out = []
+    for part in s.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out += range(int(a), int(b or a) + 1)
+    return out
+
+
+def _host_path_leg(eng, w, ch, numa):
+    import numpy as np
+    import chunkfs_amd as cfa
+    import oracle
+    hb = w.bufs[0][:w.lens[0]].cpu().numpy()  # (first touched by this thread: on its node)
     ch.chunk_array(hb)
     reps, t_h = 3, time.perf_counter()
     for _ in range(reps):
@@ -729,6 +778,7 @@ def host_path_leg(eng, w):
     t_h = (time.perf_counter() - t_h) / reps
     hp = {"GiBps": hb.size / t_h / (1 << 30), "bytes": int(hb.size), "chunks": int(hc.shape[0]),
           "entry": "cdc_chunk_data (pageable host buffer -> pinned ring -> H2D -> pipeline -> host-mapped chunk list)"}
+    hp["numa"] = numa  # (re-read after the calls below: the chunk list is allocated by the first one)
     fs_bytes = min(hb.size, 256 << 20)
     seg = 1 << 20
     ref_spans, ref_secs = oracle.fs_write("fast", hb[:fs_bytes], *eng.sizes)
@@ -774,6 +824,7 @@ def host_path_leg(eng, w):
         "metric": "bytes / wall seconds cdc_write_begin -> cdc_write_finish, 1 MiB cdc_write_segment calls "
                   "(CPU copy into the pinned ring, async H2D, device chunking of 256 MiB windows, carried chunk "
                   "in HBM)"}
+    hp["numa"] = {**numa, **cfa.host_placement(ch)}
     return hp
 
 

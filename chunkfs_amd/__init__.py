@@ -416,6 +416,16 @@ def host_stats(chunker):
             "small_calls": int(v[5]), "small_fallbacks": int(v[6])}
 
 
+def host_placement(chunker):
+    """cdc_debug_host_placement: the device's PCI address, NUMA node and link;
+    the node the pinned ring and chunk list landed on; copy-helper pinning."""
+    import json
+    buf = ctypes.create_string_buffer(1024)
+    n = lib().cdc_debug_host_placement(chunker._h, buf, 1024)
+    check(n)
+    return json.loads(buf.value.decode())
+
+
 class DedupIndex:
     """The reference's chunk Database keyed by SHA-256 digest (database.rs:74-87,
     first insert wins) with its storage statistics (storage.rs:193-240), as a

@@ -32,7 +32,7 @@ EXPORTS = [
 ]
 # include/chunkfs_amd_debug.h (diagnostics, not part of the drop-in boundary)
 DEBUG_EXPORTS = ["cdc_debug_pipeline", "cdc_debug_record_cap", "cdc_debug_copy", "cdc_debug_host_stats",
-                 "cdc_debug_read_bw",
+                 "cdc_debug_read_bw", "cdc_debug_host_placement",
                  "cdc_debug_timing_back"]
 
 
@@ -162,6 +162,8 @@ def lib():
     L.cdc_debug_record_cap.restype = ctypes.c_uint32
     L.cdc_debug_read_bw.argtypes = [P, P, sz, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     L.cdc_debug_read_bw.restype = ctypes.c_int
+    L.cdc_debug_host_placement.argtypes = [P, ctypes.c_char_p, sz]
+    L.cdc_debug_host_placement.restype = ctypes.c_int64
     L.cdc_debug_copy.argtypes = [P, ctypes.c_int, P, sz]
     L.cdc_debug_copy.restype = ctypes.c_int64
     L.cdc_version.argtypes = []

@@ -116,6 +116,11 @@ int cdc_debug_read_bw(cdc_handle_t *h, const uint8_t *d_buf, size_t len, int rep
     return h->engine->read_bw(d_buf, len, reps, ms);
 }
 
+int64_t cdc_debug_host_placement(cdc_handle_t *h, char *buf, size_t cap) {
+    if (!h || (cap && !buf)) return bad_handle();
+    return h->engine->host_placement_json(buf, cap);
+}
+
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size) {
     if (!h || !t) return (int)bad_handle();
     const cdc_timing_t &src = h->engine->timing();

@@ -263,7 +263,7 @@ int Engine::ensure_host_staging(size_t n) {
     // ++ first[n+1] (n + 32), the walk's flags[4] and fix-up round flag blocks
     // (4 x walk::kMaxFixRounds).  Slots 1-2: more FastCDC batches in flight.
     h_stage_per_ = 5 * want + 36 + 4 * walk::kMaxFixRounds;
-    HIP_TRY(hipHostMalloc(&h_stage_, kHostSlots * h_stage_per_ * sizeof(uint64_t), hipHostMallocCoherent));
+    HIP_TRY(placement().host_malloc(&h_stage_, kHostSlots * h_stage_per_ * sizeof(uint64_t), hipHostMallocCoherent));
     h_stage_streams_ = want;
     for (int k = 0; k < kSlots; ++k) fs_[k].tables.clear();
     return CDC_OK;

@@ -28,11 +28,24 @@ namespace cdc {
 // (CopyPool::shared), helpers spin briefly after a job (the next 1 MiB segment
 // usually follows within microseconds), then sleep.  copy() returns when
 // every part is done (hostpath.cpp).
+// Where the host side of the boundary runs (hostpath.cpp): the device's PCIe
+// address, NUMA node and link; the node's CPUs this process may use.
+struct HostPlacement {
+    std::string pci, link, link_max;
+    int node = -1;
+    int allowed = 0;          // CPUs in this process's affinity mask
+    std::vector<int> cpus;    // of them, those on `node`
+    bool enabled = false;     // pinned memory and copy helpers placed on `node`
+    static HostPlacement probe(int device);
+    hipError_t host_malloc(void **ptr, size_t bytes, unsigned flags) const;
+    static int node_of(const void *addr);  // NUMA node of the page at addr (-1: unknown)
+};
+
 class CopyPool {
   public:
-    CopyPool(unsigned threads, unsigned spin_us);
+    CopyPool(unsigned threads, unsigned spin_us, const std::vector<int> &cpus);
     ~CopyPool();
-    static CopyPool &shared();
+    static CopyPool &for_node(int node, const std::vector<int> &cpus);
     void copy(void *dst, const void *src, size_t n);
     // Streamed copy for the small kernel's feed: pieces of `piece` bytes,
     // claimed by the caller and the awake helpers, each announced by
@@ -41,6 +54,7 @@ class CopyPool {
     // is announced.
     void copy_feed(void *dst, const void *src, size_t n, size_t piece, volatile uint64_t *ready, uint64_t seq);
     unsigned threads() const { return (unsigned)th_.size() + 1; }
+    unsigned pinned() const { return pinned_; }
 
   private:
     void run(unsigned id);
@@ -50,6 +64,7 @@ class CopyPool {
     std::mutex m_, job_m_;
     std::condition_variable cv_;
     unsigned spin_us_ = 200;
+    unsigned pinned_ = 0;  // helpers bound to the node's CPUs
     std::atomic<uint64_t> gen_{0};
     std::atomic<bool> stop_{false}, open_{false};
     std::atomic<unsigned> active_{0};  // helpers inside the current job
@@ -90,6 +105,7 @@ class Engine {
     // Host-path statistics: calls, upload s, total s of chunk_host; chunking s
     // and segments of the current / last streaming write.
     int host_stats(double *v, size_t n) const;
+    int64_t host_placement_json(char *out, size_t cap);
     // SHA-256 of chunks of one device-resident stream (Sha256Hasher::hash).
     int sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
                       uint8_t *d_digests, hipStream_t s);
@@ -257,7 +273,10 @@ class Engine {
     static constexpr size_t kRingDirect = size_t(16) << 20;  // chunk_data above this: pageable hipMemcpyAsync
     void *h_ring_ = nullptr;
     uint8_t *h_ring_dev_ = nullptr;  // the ring as the device addresses it (small-path kernel reads)
-    CopyPool *pool_ = nullptr;  // CopyPool::shared()
+    CopyPool *pool_ = nullptr;  // CopyPool::for_node(the device's node)
+    HostPlacement place_;
+    bool place_probed_ = false;
+    const HostPlacement &placement();
     hipEvent_t ring_ev_[kRingSlots] = {};
     uint32_t ring_next_ = 0;
     // Feed words of the small path's streamed input: kFeedPieces per ring

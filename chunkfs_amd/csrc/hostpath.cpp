@@ -21,10 +21,18 @@
 // chunker here restarts at each chunk boundary and looks only forward, so a
 // window's chunks other than its last are the whole write's (SURVEY.md A.4,
 // tests/test_gpu_hostpath.py).
+#include <pthread.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <sstream>
 
 #include "engine.hpp"
 
@@ -48,25 +56,135 @@ double now_s() {
 }
 }  // namespace
 
-// ---- copy pool ----------------------------------------------------------------
+// ---- host placement ---------------------------------------------------------------
+//
+// The host side of a call is a memcpy into a pinned ring slot that the device
+// then reads over PCIe, so both belong on the GPU's NUMA node: the pinned
+// buffers are allocated with that node preferred (hipHostMallocNumaUser under
+// a thread-local MPOL_PREFERRED) and the copy helpers run on that node's CPUs
+// (those of them this process may use).  CHUNKFS_AMD_COPY_NUMA=0 turns both
+// off (A/B).  Linux sysfs gives the node and the link; a box without them
+// (node -1) keeps the default placement.
 
-CopyPool::CopyPool(unsigned threads, unsigned spin_us) : spin_us_(spin_us) {
-    for (unsigned i = 1; i < threads; ++i) th_.emplace_back([this, i] { run(i); });
+namespace {
+std::string read_line(const std::string &path) {
+    FILE *f = std::fopen(path.c_str(), "r");
+    if (!f) return "";
+    char buf[256] = {0};
+    const char *r = std::fgets(buf, sizeof buf, f);
+    std::fclose(f);
+    std::string s = r ? buf : "";
+    while (!s.empty() && (s.back() == '\n' || s.back() == ' ')) s.pop_back();
+    return s;
 }
 
-// One pool per process, shared by every handle (helpers are capped at 16
-// threads whatever the number of handles): CHUNKFS_AMD_COPY_THREADS threads
-// (default 4, the caller's included), helpers spinning CHUNKFS_AMD_COPY_SPIN_US
-// microseconds (default 200) for the next job before they sleep.
-CopyPool &CopyPool::shared() {
-    static CopyPool pool([] {
+std::vector<int> parse_cpulist(const std::string &s) {  // "0-63,128-191"
+    std::vector<int> v;
+    std::stringstream ss(s);
+    std::string part;
+    while (std::getline(ss, part, ',')) {
+        if (part.empty()) continue;
+        const size_t d = part.find('-');
+        const int a = std::atoi(part.c_str());
+        const int b = d == std::string::npos ? a : std::atoi(part.c_str() + d + 1);
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c) v.push_back(c);
+    }
+    return v;
+}
+
+constexpr int kMpolDefault = 0, kMpolPreferred = 1;
+constexpr unsigned long kMpolFNode = 1, kMpolFAddr = 2;
+
+bool numa_enabled() {
+    const char *e = std::getenv("CHUNKFS_AMD_COPY_NUMA");
+    return !e || std::atoi(e) != 0;
+}
+}  // namespace
+
+HostPlacement HostPlacement::probe(int device) {
+    HostPlacement p;
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) return p;
+    std::string id = bus;
+    for (auto &c : id) c = (char)std::tolower((unsigned char)c);
+    p.pci = id;
+    const std::string dir = "/sys/bus/pci/devices/" + id + "/";
+    const std::string node = read_line(dir + "numa_node");
+    p.node = node.empty() ? -1 : std::atoi(node.c_str());
+    p.link = read_line(dir + "current_link_speed") + " x" + read_line(dir + "current_link_width");
+    p.link_max = read_line(dir + "max_link_speed") + " x" + read_line(dir + "max_link_width");
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) == 0) {
+        p.allowed = CPU_COUNT(&allowed);
+        if (p.node >= 0)
+            for (int c : parse_cpulist(read_line("/sys/devices/system/node/node" + std::to_string(p.node) +
+                                                 "/cpulist")))
+                if (CPU_ISSET(c, &allowed)) p.cpus.push_back(c);
+    }
+    p.enabled = numa_enabled() && p.node >= 0 && !p.cpus.empty();
+    return p;
+}
+
+// Pinned host memory on the placement's node (when enabled): the calling
+// thread's policy prefers that node for this one allocation.
+hipError_t HostPlacement::host_malloc(void **ptr, size_t bytes, unsigned flags) const {
+    if (!enabled || node < 0 || node >= 1024) return hipHostMalloc(ptr, bytes, flags);
+    int old_mode = kMpolDefault;
+    unsigned long old_mask[16] = {0};
+    const bool saved = syscall(SYS_get_mempolicy, &old_mode, old_mask, 1024ul, nullptr, 0ul) == 0;
+    unsigned long mask[16] = {0};
+    mask[node / 64] = 1ul << (node % 64);
+    const bool set = syscall(SYS_set_mempolicy, kMpolPreferred, mask, 1024ul) == 0;
+    const hipError_t e = hipHostMalloc(ptr, bytes, flags | (set ? hipHostMallocNumaUser : 0u));
+    if (set) {
+        if (saved)
+            syscall(SYS_set_mempolicy, old_mode, old_mode == kMpolDefault ? nullptr : old_mask, 1024ul);
+        else
+            syscall(SYS_set_mempolicy, kMpolDefault, nullptr, 0ul);
+    }
+    return e;
+}
+
+int HostPlacement::node_of(const void *addr) {
+    if (!addr) return -1;
+    int n = -1;
+    if (syscall(SYS_get_mempolicy, &n, nullptr, 0ul, addr, kMpolFNode | kMpolFAddr) != 0) return -1;
+    return n;
+}
+
+// ---- copy pool ----------------------------------------------------------------
+
+CopyPool::CopyPool(unsigned threads, unsigned spin_us, const std::vector<int> &cpus) : spin_us_(spin_us) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c : cpus) CPU_SET(c, &set);
+    for (unsigned i = 1; i < threads; ++i) {
+        th_.emplace_back([this, i] { run(i); });
+        if (!cpus.empty() && pthread_setaffinity_np(th_.back().native_handle(), sizeof set, &set) == 0) pinned_ += 1;
+    }
+}
+
+// One pool per NUMA node, shared by every handle whose device sits on it
+// (helpers capped at 16 threads per node whatever the number of handles):
+// CHUNKFS_AMD_COPY_THREADS threads (default 4, the caller's included),
+// helpers pinned to `cpus` (the node's CPUs this process may use; empty: not
+// pinned) and spinning CHUNKFS_AMD_COPY_SPIN_US microseconds (default 200) for
+// the next job before they sleep.  Handles of one node share its pool, one
+// job at a time.
+CopyPool &CopyPool::for_node(int node, const std::vector<int> &cpus) {
+    static std::mutex m;
+    static std::map<int, std::unique_ptr<CopyPool>> pools;
+    std::lock_guard<std::mutex> g(m);
+    auto &p = pools[node];
+    if (!p) {
         const char *e = std::getenv("CHUNKFS_AMD_COPY_THREADS");
-        return (unsigned)std::max(1, std::min(e ? std::atoi(e) : 4, 16));
-    }(), [] {
-        const char *e = std::getenv("CHUNKFS_AMD_COPY_SPIN_US");
-        return (unsigned)std::max(0, std::min(e ? std::atoi(e) : 200, 100000));
-    }());
-    return pool;
+        const unsigned threads = (unsigned)std::max(1, std::min(e ? std::atoi(e) : 4, 16));
+        const char *sp = std::getenv("CHUNKFS_AMD_COPY_SPIN_US");
+        const unsigned spin = (unsigned)std::max(0, std::min(sp ? std::atoi(sp) : 200, 100000));
+        p.reset(new CopyPool(threads, spin, node >= 0 ? cpus : std::vector<int>{}));
+    }
+    return *p;
 }
 
 CopyPool::~CopyPool() {
@@ -166,15 +284,24 @@ void CopyPool::copy_feed(void *dst, const void *src, size_t n, size_t piece, vol
 
 // ---- host boundary --------------------------------------------------------------
 
+const HostPlacement &Engine::placement() {
+    if (!place_probed_) {
+        place_ = HostPlacement::probe(device_);
+        place_probed_ = true;
+    }
+    return place_;
+}
+
 int Engine::ensure_ring() {
     if (h_ring_) return CDC_OK;
-    if (!pool_) pool_ = &CopyPool::shared();
+    const HostPlacement &pl = placement();
+    if (!pool_) pool_ = &CopyPool::for_node(pl.enabled ? pl.node : -1, pl.cpus);
     // Coherent (fine-grained): the small kernel reads a slot while the host is
     // still filling it (streamed input), so the device must never cache it.
-    HIP_TRY(hipHostMalloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocCoherent));
+    HIP_TRY(pl.host_malloc(&h_ring_, kRingSlots * kRingSlot, hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_ring_dev_), h_ring_, 0));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_ready_), kRingSlots * small::kFeedPieces * 8,
-                          hipHostMallocCoherent));
+    HIP_TRY(pl.host_malloc(reinterpret_cast<void **>(&h_ready_), kRingSlots * small::kFeedPieces * 8,
+                           hipHostMallocCoherent));
     std::memset(h_ready_, 0, kRingSlots * small::kFeedPieces * 8);
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&h_ready_dev_), h_ready_, 0));
     for (auto &e : ring_ev_) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -190,7 +317,8 @@ int Engine::ensure_host_out(size_t chunks) {
     d_hout_ = nullptr;
     h_out_cap_ = 0;
     const size_t want = round_up(chunks + chunks / 8 + 64, 4096);
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_out_), want * sizeof(cdc_chunk_t), hipHostMallocMapped));
+    HIP_TRY(placement().host_malloc(reinterpret_cast<void **>(&h_out_), want * sizeof(cdc_chunk_t),
+                                    hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_hout_), h_out_, 0));
     h_out_cap_ = want;
     return CDC_OK;
@@ -475,6 +603,28 @@ int64_t Engine::write_drain(uint64_t *out, size_t cap) {
     std::memcpy(out, wr_.spans.data() + wr_.drained, k * sizeof(uint64_t));
     wr_.drained += k;
     return (int64_t)k;
+}
+
+// JSON: the device's PCI address, NUMA node and link, where the pinned ring
+// landed and how the copy helpers were placed (bench.py host_path.numa).
+int64_t Engine::host_placement_json(char *out, size_t cap) {
+    int rc = ensure_ring();
+    if (rc) return rc;
+    const HostPlacement &p = placement();
+    std::ostringstream o;
+    o << "{\"pci\": \"" << p.pci << "\", \"gpu_node\": " << p.node << ", \"link\": \"" << p.link
+      << "\", \"link_max\": \"" << p.link_max << "\", \"numa_placement\": " << (p.enabled ? "true" : "false")
+      << ", \"ring_node\": " << HostPlacement::node_of(h_ring_)
+      << ", \"chunk_list_node\": " << HostPlacement::node_of(h_out_)
+      << ", \"allowed_cpus\": " << p.allowed << ", \"node_cpus_allowed\": " << p.cpus.size()
+      << ", \"copy_threads\": " << pool_->threads() << ", \"helpers_pinned\": " << pool_->pinned() << "}";
+    const std::string s = o.str();
+    if (out && cap) {
+        const size_t k = std::min(cap - 1, s.size());
+        std::memcpy(out, s.data(), k);
+        out[k] = 0;
+    }
+    return (int64_t)s.size();
 }
 
 int Engine::host_stats(double *v, size_t n) const {

@@ -45,6 +45,16 @@ int cdc_debug_timing_back(cdc_handle_t *h, uint32_t back, cdc_timing_t *t, size_
  * roofline.frac_of_achievable. */
 int cdc_debug_read_bw(cdc_handle_t *h, const uint8_t *d_buf, size_t len, int reps, double *ms);
 
+/* Host placement of the boundary as a JSON object written into buf (cap bytes,
+ * NUL-terminated, truncated if short): the device's PCI address, NUMA node
+ * ("gpu_node", -1 unknown) and PCIe link (current and max), whether the pinned
+ * ring / chunk list / staging were allocated on that node and the copy helpers
+ * bound to its CPUs ("numa_placement"; CHUNKFS_AMD_COPY_NUMA=0 turns it off),
+ * the node the ring and chunk list actually landed on, the CPUs this process
+ * may use and how many of the helpers were pinned.  Allocates the ring if the
+ * handle has none yet.  Returns the JSON length or a negative CDC_E* code. */
+int64_t cdc_debug_host_placement(cdc_handle_t *h, char *buf, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,3 +136,31 @@ def test_low_entropy_64MiB(algo, kind, sizes):
     ref = oracle.fastcdc(data, *sizes) if algo == "fast" else oracle.cdc(algo, data, *sizes)
     _assert_same(out[:int(first[1])].cpu().numpy().view(np.uint64), ref, f"{algo} {kind} {sizes}")
     ch.close()
+
+
+@pytest.mark.parametrize("algo", ["ultra", "leap", "rabin", "seq"])
+def test_config5_full_gib_stream_avg64k(algo):
+    """Config 5 at its full stream size: one whole 1 GiB splitmix64 stream per
+    segment-walk rule at 16/64/512 KiB (min = avg/4, max = 8 avg).  The
+    size-independent invariants (exact tiling from 0, min <= len <= max but
+    the last chunk, the chunk count near n/avg) hold, and every chunk equals
+    the oracle's."""
+    import torch
+    from chunkfs_amd import _lib
+    avg = 65536
+    sizes = (avg // 4, avg, avg * 8)
+    n = 1 << 30
+    b = torch.empty(n, dtype=torch.uint8, device=DEV)
+    _lib.check(_lib.lib().cdc_fill_splitmix64_device(ctypes.c_void_p(b.data_ptr()), n, 5000, None))
+    ch = _chunker(algo, sizes)
+    first, out = _device_chunks(ch, [b], [n])
+    assert int(first[0]) == 0
+    got = out[:int(first[1])].cpu().numpy().view(np.uint64)
+    off, ln = got[:, 0].astype(np.int64), got[:, 1].astype(np.int64)
+    assert off[0] == 0 and (off[1:] == np.cumsum(ln)[:-1]).all() and int(ln.sum()) == n
+    assert (ln[:-1] >= sizes[0]).all() and (ln <= sizes[2]).all()
+    assert n // sizes[2] <= len(ln) <= n // sizes[0] + 1
+    host = b.cpu().numpy()
+    del b
+    _assert_same(got, oracle.cdc(algo, host, *sizes), f"config 5 full {algo} {sizes}")
+    ch.close()

@@ -210,3 +210,57 @@ def test_reference_1MiB_loop_through_chunk_data():
     ref, _ = oracle.fs_write("fast", data, *SIZES["fast"])
     assert spans == [int(x) for x in ref]
     ch.close()
+
+
+def test_host_placement_reported_and_followed():
+    """cdc_debug_host_placement: the device's PCI address, node and link; with
+    NUMA placement on, the pinned ring and chunk list sit on the GPU's node."""
+    import chunkfs_amd as c
+    ch = _chunker("fast")
+    p = c.host_placement(ch)
+    assert p["pci"] and p["copy_threads"] >= 1 and p["allowed_cpus"] >= 1
+    if p["numa_placement"]:
+        assert p["gpu_node"] >= 0 and p["node_cpus_allowed"] >= 1
+        assert p["ring_node"] in (p["gpu_node"], -1)  # (-1: the kernel would not say)
+        assert p["helpers_pinned"] == p["copy_threads"] - 1 or p["helpers_pinned"] == 0  # (the node's pool may predate)
+    data = oracle.splitmix64_bytes((1 << 20) + 77, 5)
+    assert (ch.chunk_array(data)[:, 1] == _whole("fast", data)).all()
+    ch.close()
+
+
+def test_chunk_data_two_handles_two_threads():
+    """Handles on one node share that node's copy pool, one job at a time:
+    two threads calling chunk_data on two handles get bit-exact chunks; the
+    small path handles the calls (a wait that outlasts the kernel's feed poll
+    becomes a fallback to the regular pipeline, still exact: counted, not
+    required to be 0)."""
+    import threading
+    import chunkfs_amd as c
+    chs = [_chunker("fast"), _chunker("fast")]
+    datas = [oracle.splitmix64_bytes((1 << 20) + 4099 * i, 40 + i) for i in range(8)]
+    refs = [_whole("fast", d) for d in datas]
+    errs = []
+    before = [c.host_stats(h) for h in chs]
+
+    def run(k):
+        try:
+            for rep in range(20):
+                i = (rep * 2 + k) % len(datas)
+                got = chs[k].chunk_array(datas[i])[:, 1]
+                if not (got.shape == refs[i].shape and (got == refs[i]).all()):
+                    errs.append((k, rep))
+        except Exception as e:  # noqa: BLE001
+            errs.append((k, repr(e)))
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    after = [c.host_stats(h) for h in chs]
+    small = sum(a["small_calls"] - b["small_calls"] for a, b in zip(after, before))
+    fb = sum(a["small_fallbacks"] - b["small_fallbacks"] for a, b in zip(after, before))
+    assert small == 40 and fb <= small
+    for h in chs:
+        h.close()
