@@ -983,6 +983,10 @@ def main(argv=None):
             extras["config5"] = c5
 
     traffic, traffic_src = traffic_for_build(args.traffic_json, bytes_rank)
+    # the same counter on the bare read kernel (tools/pmc.sh fetch_read): what
+    # a pure streaming read of these bytes fetches on this part
+    traffic_read, _ = traffic_for_build(os.path.join(os.path.dirname(args.traffic_json), "pmc_read_traffic.json"),
+                                        bytes_rank)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -1009,6 +1013,7 @@ def main(argv=None):
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_read_kernel": traffic_read,
                 "kernel": "scan_kernel (gear candidate scan)",
                 "kernel_ms": scan_avg_ms, "algorithmic_bytes_per_launch": bytes_rank,
                 "achievable_GBps": read_gbs,

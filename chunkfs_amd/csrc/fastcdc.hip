@@ -67,6 +67,13 @@ __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
 #ifndef CDC_SCAN_WAVES
 #define CDC_SCAN_WAVES 12  // as fast as 16 (profiles/r05/r05v_scan_12_waves.log), 136 KiB of LDS
 #endif
+// Span g goes to wave g / gridDim of block g % gridDim (wave-major): the
+// last, partial round of spans (16384 spans = 5.33 rounds of 3072 waves at
+// 1 GiB) then lands on a few waves of EVERY CU instead of on all the waves
+// of a third of the CUs while the other CUs idle.
+#ifndef CDC_SCAN_WAVE_MAJOR
+#define CDC_SCAN_WAVE_MAJOR 1
+#endif
 #ifndef CDC_SCAN_LOOK
 #define CDC_SCAN_LOOK 1
 #endif
@@ -574,7 +581,8 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
     Q4 A, B, C;
     uint32_t si, wb = 0;
     uint64_t off;
-    uint64_t g = next_full((uint64_t)blockIdx.x * kW + wave, si, off);
+    uint64_t g = next_full(CDC_SCAN_WAVE_MAJOR ? (uint64_t)wave * gridDim.x + blockIdx.x
+                                               : (uint64_t)blockIdx.x * kW + wave, si, off);
     const uint8_t *base = nullptr, *gp = nullptr;
     auto prefetch = [&]() {  // first two steps and the carry bytes of span g
         base = st.ptrs[si] + off;
@@ -853,7 +861,8 @@ __global__ __launch_bounds__(kDmaW * 64, 1) void scan_dma_kernel(const StreamTab
     //   otherwise:             step t+1 (4)                   -> vmcnt(4)
     uint32_t si;
     uint64_t off;
-    uint64_t g = next_full((uint64_t)blockIdx.x * kDmaW + wave, si, off);
+    uint64_t g = next_full(CDC_SCAN_WAVE_MAJOR ? (uint64_t)wave * gridDim.x + blockIdx.x
+                                               : (uint64_t)blockIdx.x * kDmaW + wave, si, off);
     const uint8_t *base = nullptr;
     if (g < st.total_spans) {
         base = stream_ptr(si) + off;

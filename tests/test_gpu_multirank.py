@@ -63,14 +63,14 @@ def test_eight_ranks_real_shard_counts():
     """The driver's 8-GPU shapes rehearsed on one GPU: `bench.py --gpus 8` with
     the real shard COUNTS (config 4: 1024 streams = 128 per rank; config 5: 16
     streams = 2 per rank) at small sizes, every rank sharing cuda:0, every
-    rank's first streams checked against the oracle (min over ranks), the
-    config-4 strong-scaling efficiency reported (rank 0 re-times the whole
+    rank's first streams checked against the oracle (min over ranks; config
+    5: the whole first streams of ranks 0 and 7), the config-4 strong-scaling efficiency reported (rank 0 re-times the whole
     1024-stream batch alone)."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--share-device",
                         "--rank-parity", "--stream-bytes", str(24 << 20), "--batch-streams", "1024",
                         "--batch-stream-bytes", str(1 << 20), "--config4-steps", "1", "--config5-streams", "16",
-                        "--config5-stream-bytes", str(8 << 20), "--config5-check", str(4 << 20), "--steps", "2",
+                        "--config5-stream-bytes", str(8 << 20), "--steps", "2",
                         "--warmup", "1", "--cpu-seconds", "0"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
@@ -85,4 +85,5 @@ def test_eight_ranks_real_shard_counts():
     c5 = line["config5"]
     assert c5["streams_per_gpu"] == 2 and len(c5["lines"]) == 12
     assert all(v["parity_vs_oracle"] is True for v in c5["lines"].values()), c5["lines"]
+    assert c5["parity_definition"].startswith("the whole first stream of rank 0 and of rank 7")
     assert "summary" in line and line["summary"]["value_GiBps"] == line["value"]

@@ -6,9 +6,9 @@ KRE=${2:-p3::.*scan_kernel}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-run() {  # name, counters...
+run() {  # name, counters...  (kernel regex: $RKRE, default $KRE)
   local name=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" --output-format csv \
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "${RKRE:-$KRE}" --output-format csv \
       -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity --no-host-path --no-algos \
       --no-sweep --no-config4 > $OUT/$name.log 2>&1
   local rc=$?
@@ -20,6 +20,9 @@ run sq2 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST
 run sq3 SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_INT64 SQ_INST_LEVEL_LDS SQ_BUSY_CU_CYCLES || exit 1
 run fetch FETCH_SIZE || exit 1
 run tcc TCC_HIT_sum TCC_MISS_sum || exit 1
+# calibration: the same counter on the bench's bare read of the stream (read_kernel,
+# the achievable-bandwidth reference), so the scan's ratio can be read against it
+RKRE="read_kernel" run fetch_read FETCH_SIZE || exit 1
 for d in $OUT/*/; do f=$(find $d -name "*counter_collection.csv" | head -1); [ -n "$f" ] && echo "== $d" && python3 - "$f" <<'PY'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -32,4 +35,6 @@ PY
 done
 f=$(find $OUT/fetch -name "*counter_collection.csv" | head -1)
 [ -n "$f" ] && python3 tools/traffic_json.py "$f" $OUT/traffic.json 1073741824
+f=$(find $OUT/fetch_read -name "*counter_collection.csv" | head -1)
+[ -n "$f" ] && python3 tools/traffic_json.py "$f" $OUT/traffic_read.json 1073741824 read_kernel
 exit 0

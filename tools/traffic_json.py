@@ -6,7 +6,9 @@ FETCH_SIZE is reported in KiB, and on gfx950 it counts exactly half of the
 bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, "HBM [CDNA4]"):
 bytes = FETCH_SIZE * 1024 * 2.
 
-usage: tools/traffic_json.py <fetch counter_collection.csv> <out.json> [workload_bytes]
+usage: tools/traffic_json.py <fetch counter_collection.csv> <out.json> [workload_bytes] [kernel]
+(kernel: "scan_kernel", the default, or "read_kernel" -- the bench's bare read of
+the same stream, whose ratio calibrates the scan's)
 
 The JSON records the library's source digest (chunkfs_amd.build.source_digest)
 so bench.py only quotes traffic measured on the build that is running.
@@ -23,17 +25,19 @@ from chunkfs_amd import build  # noqa: E402
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     workload = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 30
+    kern = sys.argv[4] if len(sys.argv) > 4 else "scan_kernel"
     vals, name = [], None
     for r in csv.DictReader(open(src)):
         # FastCDC's scan (cdc::p3::scan_kernel), not the walk engine's prefix scan
-        if r["Counter_Name"] == "FETCH_SIZE" and "p3::" in r["Kernel_Name"] and "scan_kernel" in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if r["Counter_Name"] == "FETCH_SIZE" and kern in k and (kern != "scan_kernel" or "p3::" in k):
             vals.append(float(r["Counter_Value"]))
-            name = r["Kernel_Name"]
+            name = k
     if not vals:
-        sys.exit("no scan_kernel FETCH_SIZE rows in " + src)
+        sys.exit(f"no {kern} FETCH_SIZE rows in " + src)
     per_launch = sum(vals) / len(vals) * 1024 * 2
     out = {
-        "kernel": "scan_kernel",
+        "kernel": kern,
         "kernel_symbol": name,
         "source_digest": build.source_digest(),
         "workload_bytes": workload,
