@@ -622,7 +622,14 @@ int Engine::fast_collect(int k) {
                                              : "chain overflow, output bound or look-back timeout (internal error)");
         return CDC_EDEVICE;
     }
-    if (fp_.diag & 128) {
+    if (fp_.diag & 64) {  // resolve block spans (100 MHz stamps -> us)
+        const uint64_t *d = h_misc + p3::kStatDiag0;
+        const uint64_t s0 = ~d[0], s1 = d[1], e1 = d[2], e0 = ~d[3];
+        const double blocks = (double)p3::resolve_blocks(b.spans);
+        std::fprintf(stderr, "resolve blocks, us: starts spread %.2f  first start -> first end %.2f  -> last end %.2f  "
+                             "longest block %.2f  mean block %.2f\n", (s1 - s0) / 100.0, (e0 - s0) / 100.0,
+                     (e1 - s0) / 100.0, d[4] / 100.0, d[5] / 100.0 / (blocks ? blocks : 1.0));
+    } else if (fp_.diag & 128) {
         const double waves = (double)p3::resolve_blocks(b.spans) * 8;
         std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk "
                              "lookback(w0) out):");

@@ -1032,12 +1032,18 @@ __device__ __forceinline__ uint32_t trunc_words(const uint8_t *data, uint64_t w0
     return t;
 }
 
-// The same for any chunk start, out of line: every rare caller (virtual
-// entries, exact walk steps, the dense path) shares this one copy, which
-// keeps the resolve kernel's code inside the instruction cache.  Near the
+// The same for any chunk start (virtual entries, exact walk steps, the dense
+// path; inlined since round 5, see CDC_RES_CALLS).  Near the
 // end of the stream the bytes are read one at a time (positions >= n are
 // never tested: d < len).
-__device__ __noinline__ uint32_t trunc_at(const uint8_t *data, uint64_t n, uint64_t c, uint64_t mask_s,
+// Inlined (default): the resolve kernel then has no call frames and no VGPR
+// spills, so no private segment -- no scratch set-up on its first launch
+// (0.31 ms cold with the out-of-line copies, 0.077 ms inlined) and 73-75 vs
+// 73-78 us warm (profiles/r05/r05r_*).  __noinline__ is the A/B path.
+#ifndef CDC_RES_CALLS
+#define CDC_RES_CALLS __forceinline__
+#endif
+__device__ CDC_RES_CALLS uint32_t trunc_at(const uint8_t *data, uint64_t n, uint64_t c, uint64_t mask_s,
                                           uint64_t mask_l, uint32_t mn, uint32_t avg, uint32_t mx, uint32_t trunc,
                                           lds_u64 *tab) {
     if (n - c <= mn) return kTruncNone;
@@ -1065,9 +1071,16 @@ __device__ __forceinline__ uint32_t trunc_call(const uint8_t *data, uint64_t n, 
 // Exact next start from the bytes alone, wave-cooperative (64 positions per
 // step: one coalesced byte load + a 6-step shuffle prefix scan).  For chains
 // that cross an overflowed record list.  Wave-uniform arguments.
-__device__ __noinline__ uint64_t coop_next_bytes(const FastParams fp, const uint64_t *tab, const uint8_t *data,
+// (Scalar parameters, not the FastParams aggregate, which would go through a
+// stack frame if this were out of line.)
+__device__ CDC_RES_CALLS uint64_t coop_next_bytes(uint32_t mn, uint32_t avg, uint32_t mx, uint64_t mask_s,
+                                                 uint64_t mask_l, const uint64_t *tab, const uint8_t *data,
                                                  uint64_t n, uint64_t s, uint32_t lane) {
-    if (n - s <= fp.min) return n;
+    if (n - s <= mn) return n;
+    FastParams fp{};
+    fp.min = mn;
+    fp.avg = avg;
+    fp.max = mx;
     const Regime R = regime(fp, s, n);
     uint64_t h = 0;
     for (uint64_t b = R.a0; b < R.re; b += 64) {
@@ -1076,7 +1089,7 @@ __device__ __noinline__ uint64_t coop_next_bytes(const FastParams fp, const uint
         const bool in = p < p1;
         const uint64_t gv = in ? tab[as_global1(data)[s + p]] : 0;
         const uint64_t x = gear_prefix(gv, lane) + ((h << lane) << 1);
-        const bool hit = in && !(x & (p < R.ce ? fp.mask_s : fp.mask_l));
+        const bool hit = in && !(x & (p < R.ce ? mask_s : mask_l));
         const uint64_t m = __ballot(hit);
         if (m) return s + b + (uint64_t)(__ffsll((long long)m) - 1);
         h = __shfl(x, (int)(p1 - b - 1));
@@ -1165,7 +1178,7 @@ __device__ __forceinline__ void walk_lanes(const StreamTable &st, const FastPara
             const int l = __ffsll((long long)m) - 1;
             const uint64_t sl = readlane_u64(s, l), nl = readlane_u64(L.n, l);
             const uint8_t *dl = reinterpret_cast<const uint8_t *>(readlane_u64(reinterpret_cast<uint64_t>(L.data), l));
-            const uint64_t nx = coop_next_bytes(fp, tab, dl, nl, sl, lane);
+            const uint64_t nx = coop_next_bytes(fp.min, fp.avg, fp.max, fp.mask_s, fp.mask_l, tab, dl, nl, sl, lane);
             if ((int)lane == l) {
                 s = nx;
                 go = s < L.span_end;
@@ -1240,6 +1253,7 @@ struct BlockState {
     uint32_t N[kBlockSpans];  // starts in the span
     uint8_t F[kBlockSpans];   // 1: the span starts a stream
     uint64_t b, base, pred;
+    uint64_t t0;              // entry stamp (diag & 64)
     uint32_t rewalk;
     uint64_t stat[kResWaves][3];  // per wave: candidates << 24 | overflowed, re-walks, exact steps
     uint64_t diag[kResWaves][kStatDiagN];  // per wave phase times (diag & 128)
@@ -1714,6 +1728,7 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
     // Blocks take their index in dispatch order, so the look-back only ever
     // waits on blocks that are already running or done.
     if (threadIdx.x == 0) {
+        if (fp.diag & 64) B.t0 = __builtin_amdgcn_s_memrealtime();
         B.b = atomicAdd((unsigned long long *)&cp.stats[kStatOrder], 1ull);
         B.base = B.pred = 0;
         B.rewalk = 0;
@@ -1991,7 +2006,16 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
             rw += B.stat[w][1];
             sp += B.stat[w][2];
         }
-        if (fp.diag & 128)
+        if (fp.diag & 64) {  // block spans (100 MHz stamps): min / max start, max / min end, max / sum duration
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime(), t0 = B.t0;
+            unsigned long long *d = (unsigned long long *)&cp.stats[kStatDiag0];
+            atomicMax(d + 0, (unsigned long long)~t0);
+            atomicMax(d + 1, (unsigned long long)t0);
+            atomicMax(d + 2, (unsigned long long)t1);
+            atomicMax(d + 3, (unsigned long long)~t1);
+            atomicMax(d + 4, (unsigned long long)(t1 - t0));
+            atomicAdd(d + 5, (unsigned long long)(t1 - t0));
+        } else if (fp.diag & 128)
             for (int k = 0; k < kStatDiagN; ++k) {
                 uint64_t d = 0;
                 for (int w = 0; w < kResWaves; ++w) d += B.diag[w][k];

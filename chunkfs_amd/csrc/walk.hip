@@ -2116,6 +2116,26 @@ __global__ __launch_bounds__(kWalkBlock) void bits_kernel(const StreamTable st, 
 #ifndef CDC_RABIN_SKEW
 #define CDC_RABIN_SKEW 0  // measured slower: 1262 vs 1346 GiB/s (profiles/r05/r05g_rabin_*.log)
 #endif
+// The leaving byte's term after the shift (CDC_RABIN_OUT2=1): d' = ((d << 8) |
+// in) ^ mod[top(d)] ^ out2[leaving], out2[b] = b x^(8W) mod P (= x^8 out[b]),
+// so the out lookup is off the digest's dependency chain and both table
+// values fold in with one v_xor3 per half: 7 VALU per byte for the digest
+// instead of 11 (the round-4 PMC had the pass VALU-issue-bound at 14.7 per byte).
+#ifndef CDC_RABIN_OUT2
+#define CDC_RABIN_OUT2 0  // measured slower: rbits 0.58-0.60 vs 0.55-0.57 ms (profiles/r05/r05q_*)
+#endif
+// A wave hashes 2^CDC_RABIN_GROUP_LOG2 consecutive pieces of one segment as
+// one range (2 KiB per lane at 32 KiB pieces instead of 512 B): the 48-byte
+// warm-up each lane re-hashes before its range drops from 9.4 % to 2.3 % of
+// the bytes.
+#ifndef CDC_RABIN_GROUP_LOG2
+#define CDC_RABIN_GROUP_LOG2 0  // measured slower at 2: rbits 0.60 vs 0.55-0.57 ms (profiles/r05/r05q_*)
+#endif
+static_assert(CDC_RABIN_GROUP_LOG2 <= 2, "rbits_kernel: a lane's quiet bits are one 32-bit word (<= 2 KiB per lane)");
+__host__ __device__ __forceinline__ uint32_t rabin_group_log2(const StreamTable &st, const WalkParams &wp) {
+    const uint32_t k = st.span_log2 - wp.piece_log2;
+    return k < CDC_RABIN_GROUP_LOG2 ? k : CDC_RABIN_GROUP_LOG2;
+}
 constexpr int kRabinReps = CDC_RABIN_REPS;
 constexpr int kRabinWaves = CDC_RABIN_WAVES;  // pieces per block (64 KiB of tables shared by 8 waves)
 
@@ -2141,13 +2161,16 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     static_assert(kRabinReps == 16, "rbits_kernel: 16 replicas per table");
     for (int i = threadIdx.x; i < 256 * 32; i += 64 * kRabinWaves) {
         const int e = i >> 5, k = i & 31;
-        rt[i] = wp.tabs[(k < 16 ? 0 : 256) + e];
+        uint64_t v = wp.tabs[(k < 16 ? 0 : 256) + e];
+        if (CDC_RABIN_OUT2 && k >= 16) v = (v << 8) ^ wp.tabs[v >> wp.rabin_shift];  // x^8 out[e] mod P
+        rt[i] = v;
     }
 #endif
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     Piece pc;
-    if (!piece_of(st, wp, (uint64_t)blockIdx.x * kRabinWaves + wave_id(), pc)) return;
+    const uint32_t grp = rabin_group_log2(st, wp);
+    if (!piece_of(st, wp, ((uint64_t)blockIdx.x * kRabinWaves + wave_id()) << grp, pc)) return;
 #if CDC_RABIN_SKEW
     const uint32_t om = (lane & 15) * 8, oo = 256 * kStride + om;  // this lane's mod / out replica
 #else
@@ -2156,7 +2179,9 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
     lds_wchar *tb = (lds_wchar *)rt;
     const uint64_t len = st.lens[pc.si];
     const uint8_t *base = st.ptrs[pc.si];
-    const uint64_t w = (1ull << wp.piece_log2) >> 6;  // bytes per lane (a multiple of 64)
+    // bytes per lane (a multiple of 64; the group's pieces are consecutive in
+    // the segment, in bytes and in bitmap words)
+    const uint64_t w = (1ull << (wp.piece_log2 + grp)) >> 6;
     const uint64_t p0 = pc.off + lane * w;
     uint32_t qm = 0, qa = 0;  // bit i: word i of the lane's range has no hit / only hits (quiet runs)
     if (p0 < len) {
@@ -2174,6 +2199,13 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
                 const uint32_t ao = __builtin_amdgcn_perm(oo, ow, 0x0c0c0004u | ((uint32_t)(j & 3) << 8));
 #endif
                 const uint64_t o = *reinterpret_cast<lds_w64 *>(tb + ao);
+#if CDC_RABIN_OUT2 && !CDC_RABIN_SKEW
+                // o = out2[leaving byte], folded in after the shift (off the chain)
+                const uint64_t m = *reinterpret_cast<lds_w64 *>(tb + (((hi >> tsh) << 8) | om));
+                hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32) ^ (uint32_t)(o >> 32);
+                // (lo << 8) | the entering byte, one v_perm
+                lo = __builtin_amdgcn_perm(lo, cw, 0x06050400u | (uint32_t)(j & 3)) ^ (uint32_t)m ^ (uint32_t)o;
+#else
                 lo ^= (uint32_t)o;
                 hi ^= (uint32_t)(o >> 32);
 #if CDC_RABIN_SKEW
@@ -2182,8 +2214,8 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
                 const uint64_t m = *reinterpret_cast<lds_w64 *>(tb + (((hi >> tsh) << 8) | om));
 #endif
                 hi = __builtin_amdgcn_alignbit(hi, lo, 24) ^ (uint32_t)(m >> 32);
-                // (lo << 8) | the entering byte, one v_perm
                 lo = __builtin_amdgcn_perm(lo, cw, 0x06050400u | (uint32_t)(j & 3)) ^ (uint32_t)m;
+#endif
                 if (test) bits |= min(lo & rmask, 1u) << (sh + j);
             }
         };
@@ -2220,7 +2252,15 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
             qa |= (uint32_t)(hits == ~0ull) << ((a - p0) >> 6);
         }
     }
-    if (wp.rsum) {  // the lanes' quiet bits into summary bytes (nw words per lane, 8 / nw lanes per byte)
+    if (wp.rsum && (w >> 6) >= 8) {  // nw >= 8 words per lane: nw / 8 whole summary bytes per kind
+        const uint32_t nw = (uint32_t)(w >> 6);
+        const uint64_t W = pc.wbase + lane * nw;
+        uint8_t *b = reinterpret_cast<uint8_t *>(wp.rsum) + (W >> 6) * 16 + ((W >> 3) & 7);
+        for (uint32_t k = 0; k < nw / 8; ++k) {
+            b[k] = (uint8_t)(qm >> (8 * k));
+            b[8 + k] = (uint8_t)(qa >> (8 * k));
+        }
+    } else if (wp.rsum) {  // the lanes' quiet bits into summary bytes (nw words per lane, 8 / nw lanes per byte)
         const uint32_t nw = (uint32_t)(w >> 6), gl = 8 / nw;
         uint32_t v = (qm | qa << 8) << (nw * (lane & (gl - 1)));
         for (uint32_t o = 1; o < gl; o <<= 1) v |= (uint32_t)__shfl_xor((int)v, (int)o);
@@ -2647,7 +2687,8 @@ hipError_t launch_bits(const StreamTable &st, const WalkParams &wp, hipStream_t 
     const uint64_t pieces = st.total_spans << (st.span_log2 - wp.piece_log2);
     const unsigned blocks = (unsigned)pieces;
     if (wp.algo == 2 && wp.rabin_mask <= 0xFFFFFFFFull && wp.rabin_shift >= 32 && wp.piece_log2 >= 12)
-        rbits_kernel<<<(unsigned)((pieces + kRabinWaves - 1) / kRabinWaves), 64 * kRabinWaves, 0, s>>>(st, wp);
+        rbits_kernel<<<(unsigned)(((pieces >> rabin_group_log2(st, wp)) + kRabinWaves - 1) / kRabinWaves),
+                       64 * kRabinWaves, 0, s>>>(st, wp);
     else if (wp.algo == 2) bits_kernel<2><<<blocks, kWalkBlock, 0, s>>>(st, wp);
     else if (wp.algo == 4 && wp.bits_fine && wp.piece_log2 >= 12)
         ubits_kernel<<<(unsigned)((pieces + 3) / 4), 256, 0, s>>>(st, wp);
