@@ -183,8 +183,11 @@ class DeviceEngine:
     def timings(self, k):
         """HIP-event timings of the last k batches (oldest first), read after
         the timed loop from the engine's event ring (no per-step event wait
-        inside the loop; include/chunkfs_amd_debug.h)."""
-        return [self.ch.timing_back(b) for b in range(min(k, 64) - 1, -1, -1)]
+        inside the loop; include/chunkfs_amd_debug.h).  Async batches carry
+        events one in four (CHUNKFS_AMD_EVENT_EVERY; an event costs the stream
+        ~4 us): the timed steps' sampled batches."""
+        allt = [self.ch.timing_back(b) for b in range(min(k, 64) - 1, -1, -1)]
+        return [t for t in allt if t["total_ms"] > 0] or allt
 
     def sync(self):
         self.ch.batch_sync()

@@ -112,6 +112,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         fp.mask_s_sh = fp.mask_s << fp.tshift;
         fp.mask_l_sh = fp.mask_l << fp.tshift;
         if (const char *d = std::getenv("CHUNKFS_AMD_DIAG")) fp.diag = (uint32_t)std::atoi(d);
+        if (const char *v = std::getenv("CHUNKFS_AMD_EVENT_EVERY")) e->event_every_ = std::max(1, std::atoi(v));
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
         e->small_span_log2_ = l2 > 14 ? l2 : 14;
@@ -394,7 +395,11 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
         if (r < 0) return r;
     }
     if (pipe) {
-        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s);
+        // (async batches: the start / split / end events that cdc_last_timing
+        // reads are recorded on every event_every_-th batch only -- each
+        // event costs the stream ~4 us, r05t)
+        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s,
+                                      !async || fb_seq_ % event_every_ == 0);
         if (r < 0 || async) return r;
         return fast_drain();
     }
@@ -417,7 +422,7 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
         // (kSmallFallback: the regular pipeline below)
     }
     if (algo_ == CDC_ALGO_FASTCDC) {  // small batches: one scan + resolve, waited for here
-        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s);
+        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s, true);
         if (r < 0) return r;
         return fast_drain();
     }
@@ -471,7 +476,7 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
 // the resolve launches; no host wait.  The host collects it (fast_collect)
 // when its stats block is needed again or at fast_drain().
 int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
-                            size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s) {
+                            size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s, bool timed) {
     if (fb_any_ && s != fb_stream_) {  // one pipeline per stream
         const int64_t r = fast_drain();
         if (r < 0) return r;
@@ -562,13 +567,15 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     rec.bytes = bytes;
     rec.spans = spans;
     hipEvent_t *ev = tev_[seq % kTimeRing];
-    HIP_TRY(hipEventRecord(ev[0], s));
+    tev_timed_[seq % kTimeRing] = timed;
+    rec.timed = timed;
+    if (timed) HIP_TRY(hipEventRecord(ev[0], s));
     if (spans)
         HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails, num_cus_,
                                 s));
-    HIP_TRY(hipEventRecord(ev[1], s));
+    if (timed) HIP_TRY(hipEventRecord(ev[1], s));
     if (spans) HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, s));
-    HIP_TRY(hipEventRecord(ev[2], s));
+    if (timed) HIP_TRY(hipEventRecord(ev[2], s));
     fb_seq_ = seq + 1;
     fast_batches_ = fb_seq_;
     fb_any_ = true;
@@ -615,7 +622,10 @@ int Engine::fast_collect(int k) {
         const auto t_spin = std::chrono::steady_clock::now();
         while (*done == ~0ull && std::chrono::steady_clock::now() - t_spin < budget) __builtin_ia32_pause();
     }
-    if (h_misc[p3::kStatDone] == ~0ull) HIP_TRY(hipEventSynchronize(tev_[b.seq % kTimeRing][2]));
+    if (h_misc[p3::kStatDone] == ~0ull) {  // (slow batch or a failure: wait for the stream itself)
+        if (b.timed) HIP_TRY(hipEventSynchronize(tev_[b.seq % kTimeRing][2]));
+        else HIP_TRY(hipStreamSynchronize(fb_stream_));
+    }
     b.live = false;
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
         set_error(h_misc[p3::kStatDone] != 1 ? "resolve kernel did not report back"
@@ -626,9 +636,10 @@ int Engine::fast_collect(int k) {
         const uint64_t *d = h_misc + p3::kStatDiag0;
         const uint64_t s0 = ~d[0], s1 = d[1], e1 = d[2], e0 = ~d[3];
         const double blocks = (double)p3::resolve_blocks(b.spans);
-        std::fprintf(stderr, "resolve blocks, us: starts spread %.2f  first start -> first end %.2f  -> last end %.2f  "
-                             "longest block %.2f  mean block %.2f\n", (s1 - s0) / 100.0, (e0 - s0) / 100.0,
-                     (e1 - s0) / 100.0, d[4] / 100.0, d[5] / 100.0 / (blocks ? blocks : 1.0));
+        std::fprintf(stderr, "resolve blocks, us: scan's last block end -> first start %.2f  starts spread %.2f  "
+                             "first start -> first end %.2f  -> last end %.2f  longest block %.2f  mean block %.2f\n",
+                     ((double)s0 - (double)d[6]) / 100.0, (s1 - s0) / 100.0, (e0 - s0) / 100.0, (e1 - s0) / 100.0,
+                     d[4] / 100.0, d[5] / 100.0 / (blocks ? blocks : 1.0));
     } else if (fp_.diag & 128) {
         const double waves = (double)p3::resolve_blocks(b.spans) * 8;
         std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk "
@@ -787,6 +798,10 @@ int Engine::timing_back(uint32_t back, cdc_timing_t &out) {
     hipEvent_t *ev = tev_[(fast_batches_ - 1 - back) % kTimeRing];
     float t01 = 0, t12 = 0, t02 = 0;
     HIP_TRY(hipSetDevice(device_));
+    if (!tev_timed_[(fast_batches_ - 1 - back) % kTimeRing]) {  // an async batch recorded without events
+        out.scan_ms = out.resolve_ms = out.total_ms = 0;
+        return CDC_OK;
+    }
     HIP_TRY(hipEventSynchronize(ev[2]));
     HIP_TRY(hipEventElapsedTime(&t01, ev[0], ev[1]));
     HIP_TRY(hipEventElapsedTime(&t12, ev[1], ev[2]));

@@ -159,7 +159,7 @@ class Engine {
     int64_t batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
                          size_t out_cap, uint64_t *first, hipStream_t stream, bool async);
     int64_t fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
-                        size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s);
+                        size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s, bool timed);
     int fast_collect(int rec);
     int64_t fast_drain();
     // One small FastCDC stream in one launch (small.hip): CDC_OK, kSmallFallback
@@ -240,13 +240,15 @@ class Engine {
     // scan + resolve enqueued at submit, collected (done word, first[]) by the
     // submit three later or by fast_drain.
     struct FastBatch {
-        bool live = false, resolved = false;
+        bool live = false, resolved = false, timed = true;
         int slot = 0;                // device slot
         uint64_t *h = nullptr;       // host staging block (slot seq % kHostSlots)
         size_t n = 0;
         uint64_t *first = nullptr;  // the caller's first[n+1]
         uint64_t seq = 0, bytes = 0, spans = 0;
     } fb_[3];
+    int event_every_ = 4;           // async FastCDC batches with events: 1 in event_every_ (CHUNKFS_AMD_EVENT_EVERY)
+    bool tev_timed_[kTimeRing] = {};  // events recorded for ring slot
     uint64_t timing_seq_ = 0;       // the batch timing_ describes
     uint64_t fb_seq_ = 0;           // batches submitted
     hipStream_t fb_stream_ = nullptr;  // the stream of the batches in flight

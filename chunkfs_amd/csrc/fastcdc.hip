@@ -656,6 +656,12 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         }
         flush_span(g_cur, base_cur, (uint32_t)span, avail_cur, sub - 1, ne, E, tab, rep, fp, cand, lane);
     }
+    if (fp.diag & 64) {  // the last block's end (100 MHz stamp) for the resolve's block-span report
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax((unsigned long long *)&cp.stats[kStatDiag0 + 6],
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 // ---- scan, LDS-DMA input landing (A/B path: CHUNKFS_AMD_DIAG bit 10) ---------

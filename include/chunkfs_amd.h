@@ -186,7 +186,9 @@ typedef struct cdc_timing {
     uint64_t walk_fallback_steps; /* chain-walk steps without a precomputed record link */
 } cdc_timing_t;
 
-/* Copies min(t_size, sizeof(cdc_timing_t)) bytes: pass sizeof(cdc_timing_t)
+/* Kernel times (HIP events) of the last batch; a batch enqueued by
+ * cdc_chunk_batch_device_async carries events one in four (0 ms otherwise).
+ * Copies min(t_size, sizeof(cdc_timing_t)) bytes: pass sizeof(cdc_timing_t)
  * of the header the caller was built with, so an older (shorter) struct is
  * never overrun when fields are appended in a later version. */
 int cdc_last_timing(const cdc_handle_t *h, cdc_timing_t *t, size_t t_size);

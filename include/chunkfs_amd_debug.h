@@ -36,6 +36,9 @@ int cdc_debug_host_stats(const cdc_handle_t *h, double *v, size_t n);
  * are the last batch's).  Each batch records its HIP events in its own slot of
  * a 64-entry ring, so a caller timing many back-to-back batches reads them
  * after the loop instead of waiting on each batch's events inside it.
+ * Synchronous batches always record events; batches of
+ * cdc_chunk_batch_device_async record them one in four
+ * (CHUNKFS_AMD_EVENT_EVERY=k: one in k), the others report 0 ms.
  * CDC_EINVAL when that batch is not in the ring. */
 int cdc_debug_timing_back(cdc_handle_t *h, uint32_t back, cdc_timing_t *t, size_t t_size);
 /* Measured-achievable HBM read rate on the handle's device: a read-only

@@ -114,3 +114,24 @@ def test_async_other_algorithms_are_synchronous():
     ref = oracle.cdc("rabin", b[:n].cpu().numpy(), *SIZES)
     assert got.shape == ref.shape and (got == ref).all()
     ch.close()
+
+
+def test_async_batches_sample_events():
+    """Async batches record their HIP events one in four (an event costs the
+    stream ~4 us); synchronous ones always do.  The unsampled report 0 ms."""
+    import torch
+    import chunkfs_amd as c
+    ch = c.FastChunker(c.SizeParams(*SIZES))
+    n = 24 << 20
+    buf = _dev_stream(torch, n, 11)
+    cap = ch.batch_max_chunks([n])
+    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda:0")
+    for _ in range(8):
+        ch.chunk_batch_device_async([buf.data_ptr()], [n], out.data_ptr(), cap)
+    ch.batch_sync()
+    hist = [ch.timing_back(k) for k in range(8)]
+    timed = [h for h in hist if h["total_ms"] > 0]
+    assert len(timed) == 2 and all(h["scan_ms"] > 0 and h["resolve_ms"] > 0 for h in timed)
+    ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
+    assert ch.last_timing()["scan_ms"] > 0
+    ch.close()
