@@ -63,6 +63,8 @@ class cdc_timing_t(ctypes.Structure):
         ("bytes", ctypes.c_uint64),
         ("hash_ms", ctypes.c_double),
         ("walk_fallback_steps", ctypes.c_uint64),
+        ("path", ctypes.c_uint32),   # CDC_PATH_*: 0 pipeline, 1 small kernel, 2 walk, 3 fixed, 4 empty
+        ("timed", ctypes.c_uint32),  # 1: the *_ms fields are HIP-event measurements
     ]
 
 

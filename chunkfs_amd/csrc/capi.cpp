@@ -222,7 +222,7 @@ int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes) {
     return h->engine->debug_copy(what, out, max_bytes);
 }
 
-const char *cdc_version(void) { return "chunkfs_amd 0.3 gfx950 abi 2"; }
+const char *cdc_version(void) { return "chunkfs_amd 0.5 gfx950 abi 3"; }
 
 uint32_t cdc_abi_version(void) { return CHUNKFS_AMD_ABI_VERSION; }
 

@@ -408,6 +408,7 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
     timing_ = cdc_timing_t{};
     timing_.hash_ms = hash_ms;
     timing_.bytes = bytes;
+    timing_.path = CDC_PATH_EMPTY;
     out_cap_ = out_cap;
     if (n == 0) {
         if (first) first[0] = 0;
@@ -417,7 +418,10 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
     if (rc) return rc;
     if (algo_ == CDC_ALGO_FASTCDC && n == 1 && !small_skip_ && small_ok(lens[0])) {
         rc = run_small(d_streams[0], lens[0], d_out, out_cap, first, s);
-        if (rc == CDC_OK) return (int64_t)first[1];
+        if (rc == CDC_OK) {
+            timing_.path = CDC_PATH_SMALL;  // (no events on the call path: timed stays 0)
+            return (int64_t)first[1];
+        }
         if (rc < 0) return rc;
         // (kSmallFallback: the regular pipeline below)
     }
@@ -662,6 +666,8 @@ int Engine::fast_collect(int k) {
     timing_.overflow_spans = (uint32_t)h_misc[p3::kStatOvf];
     timing_.fixup_iterations = (uint32_t)h_misc[p3::kStatRewalk];
     timing_.walk_fallback_steps = h_misc[p3::kStatOnDemand];
+    timing_.path = CDC_PATH_PIPELINE;
+    timing_.timed = b.timed ? 1u : 0u;
     timing_pending_ = true;
     timing_seq_ = b.seq;
     return CDC_OK;
@@ -798,7 +804,9 @@ int Engine::timing_back(uint32_t back, cdc_timing_t &out) {
     hipEvent_t *ev = tev_[(fast_batches_ - 1 - back) % kTimeRing];
     float t01 = 0, t12 = 0, t02 = 0;
     HIP_TRY(hipSetDevice(device_));
-    if (!tev_timed_[(fast_batches_ - 1 - back) % kTimeRing]) {  // an async batch recorded without events
+    out.path = CDC_PATH_PIPELINE;
+    out.timed = tev_timed_[(fast_batches_ - 1 - back) % kTimeRing] ? 1u : 0u;
+    if (!out.timed) {  // an async batch recorded without events
         out.scan_ms = out.resolve_ms = out.total_ms = 0;
         return CDC_OK;
     }
@@ -832,6 +840,8 @@ int Engine::run_fixed(const StreamTable &st, size_t n, const uint64_t *lens,
     HIP_TRY(hipEventElapsedTime(&t03, ev_[0], ev_[3]));
     timing_.total_ms = t03;
     timing_.scan_ms = t03;
+    timing_.path = CDC_PATH_FIXED;
+    timing_.timed = 1;
     return CDC_OK;
 }
 
@@ -1383,6 +1393,8 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     timing_.total_ms = t02;
     timing_.fixup_iterations = (uint32_t)rewalked;
     timing_.overflow_spans = settled ? 0u : 1u;
+    timing_.path = CDC_PATH_WALK;
+    timing_.timed = 1;
     return CDC_OK;
 }
 

@@ -26,8 +26,10 @@ extern "C" {
 #endif
 
 /* 2: cdc_last_timing takes the caller's sizeof(cdc_timing_t) (the struct
- *    may grow; fields are only ever appended); cdc_abi_version(). */
-#define CHUNKFS_AMD_ABI_VERSION 2
+ *    may grow; fields are only ever appended); cdc_abi_version().
+ * 3: cdc_timing_t.path / .timed appended; cdc_chunk_batch_device_async,
+ *    cdc_batch_sync. */
+#define CHUNKFS_AMD_ABI_VERSION 3
 
 /* Chunk{offset,length} -- reference src/lib.rs:43-47 (usize fields; u64 here). */
 typedef struct cdc_chunk {
@@ -184,7 +186,16 @@ typedef struct cdc_timing {
     uint64_t bytes;          /* input bytes of the batch */
     double hash_ms;          /* last cdc_sha256_chunks_device / cdc_chunk_and_hash kernel time */
     uint64_t walk_fallback_steps; /* chain-walk steps without a precomputed record link */
+    uint32_t path;           /* CDC_PATH_*: which engine path ran the batch */
+    uint32_t timed;          /* 1: the *_ms fields were measured (HIP events); 0: not timed */
 } cdc_timing_t;
+
+/* cdc_timing_t.path */
+#define CDC_PATH_PIPELINE 0 /* FastCDC scan + resolve */
+#define CDC_PATH_SMALL 1    /* FastCDC one-launch small-stream kernel (not timed: no events on its call path) */
+#define CDC_PATH_WALK 2     /* Rabin / Ultra / Leap / Seq segment-walk engine */
+#define CDC_PATH_FIXED 3    /* FSChunker */
+#define CDC_PATH_EMPTY 4    /* a batch of no streams */
 
 /* Kernel times (HIP events) of the last batch; a batch enqueued by
  * cdc_chunk_batch_device_async carries events one in four (0 ms otherwise).
@@ -285,7 +296,7 @@ int cdc_index_stats(const cdc_index_t *ix, cdc_index_stats_t *out);
 int cdc_fill_splitmix64_device(uint8_t *d_buf, size_t len, uint64_t seed,
                                void *hip_stream);
 
-/* Engine build info, e.g. "chunkfs_amd 0.3 gfx950 abi 2". */
+/* Engine build info, e.g. "chunkfs_amd 0.5 gfx950 abi 3". */
 const char *cdc_version(void);
 
 /* CHUNKFS_AMD_ABI_VERSION of the loaded library (compare with the header's). */

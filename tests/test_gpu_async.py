@@ -132,6 +132,7 @@ def test_async_batches_sample_events():
     hist = [ch.timing_back(k) for k in range(8)]
     timed = [h for h in hist if h["total_ms"] > 0]
     assert len(timed) == 2 and all(h["scan_ms"] > 0 and h["resolve_ms"] > 0 for h in timed)
+    assert sum(h["timed"] for h in hist) == 2 and all(h["path"] == 0 for h in hist)
     ch.chunk_batch_device([buf.data_ptr()], [n], out.data_ptr(), cap)
     assert ch.last_timing()["scan_ms"] > 0
     ch.close()

@@ -92,6 +92,8 @@ def test_small_reference_loop_1MiB_segments():
     # descheduled host thread) falls back to the pipeline, exact all the same:
     # a few are tolerated, not required to be 0
     assert st1["small_calls"] - st0["small_calls"] == 33
+    t = ch.last_timing()
+    assert t["path"] in (1, 0) and (t["path"] == 0 or t["timed"] == 0)  # small kernel: not timed, said so
     assert st1["small_fallbacks"] - st0["small_fallbacks"] <= 3
     ch.close()
 
