@@ -56,6 +56,10 @@ __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
     const u32x4 v = *p;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+__device__ __forceinline__ uint4 ld16_nt(g_u32x4 *p) {  // streaming hint: the line is done with
+    const u32x4 v = __builtin_nontemporal_load(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // Experiment builds (tools/scan_variants.sh) may override the scheduling
 // fences, the lookahead and the waves per CU; defaults are the measured best.
@@ -71,6 +75,9 @@ __device__ __forceinline__ uint4 ld16(g_u32x4 *p) {
 // last, partial round of spans (16384 spans = 5.33 rounds of 3072 waves at
 // 1 GiB) then lands on a few waves of EVERY CU instead of on all the waves
 // of a third of the CUs while the other CUs idle.
+#ifndef CDC_SCAN_NT_ODD
+#define CDC_SCAN_NT_ODD 0
+#endif
 #ifndef CDC_SCAN_WAVE_MAJOR
 #define CDC_SCAN_WAVE_MAJOR 1
 #endif
@@ -385,9 +392,15 @@ __device__ __forceinline__ void process_step_d(const Q4 &C, uint64_t &h, uint32_
 // The 4 coalesced loads of step t: instruction i reads piece (lane%4) of the
 // step of segment 16 i + rsel(lane/4) (16 complete 64-byte pieces per
 // instruction; rsel: see the kernel).
+// Step t reads bytes [64 t, 64 t + 64) of every 1 KiB row: the first half of
+// a 128-byte line at even t, its second half at odd t (ring B).  kNt marks the
+// second-half loads non-temporal (CDC_SCAN_NT_ODD, A/B) so that lines whose
+// first half is still waiting keep their place in L2.
+template <bool kNt = false>
 __device__ __forceinline__ void gload_step(Q4 &X, const uint8_t *gp, uint64_t istride, uint32_t t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) X.q[i] = ld16(as_global4(gp + i * istride + t * kStep));
+    for (int i = 0; i < 4; ++i)
+        X.q[i] = kNt ? ld16_nt(as_global4(gp + i * istride + t * kStep)) : ld16(as_global4(gp + i * istride + t * kStep));
 }
 
 // Transpose through the wave's LDS tile: row o (80 bytes: 64 data + 16 pad)
@@ -591,7 +604,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         if (off != 0 && lane < 48) wb = as_global1(base)[(int)lane - 48];
         gload_step(A, gp, istride, 0);
         SCHED_FENCE();
-        gload_step(B, gp, istride, 1);
+        gload_step<(bool)CDC_SCAN_NT_ODD>(B, gp, istride, 1);
         SCHED_FENCE();
     };
     if (g < st.total_spans) prefetch();
@@ -621,7 +634,7 @@ __global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, 
         CDC_PROC(lo + (T) * kStep);                                                            \
         SCHED_FENCE();                                                                         \
         stage_step(C, B, wrow, rrow);                                                          \
-        if (LOAD_B && kMode != 2) gload_step(B, gp, istride, (T) + 3);                         \
+        if (LOAD_B && kMode != 2) gload_step<(bool)CDC_SCAN_NT_ODD>(B, gp, istride, (T) + 3);  \
         SCHED_FENCE();                                                                         \
         CDC_PROC(lo + ((T) + 1) * kStep);                                                      \
         SCHED_FENCE();                                                                         \

@@ -39,8 +39,8 @@ for rep in range(3):
     ch.batch_sync()
     torch.cuda.synchronize()
     ta = (time.perf_counter() - t0) / steps
-    tims = [ch.timing_back(k) for k in range(min(steps, 60))]
-    sc = sum(t["scan_ms"] for t in tims) / len(tims)
+    tims = [t for t in (ch.timing_back(k) for k in range(min(steps, 60))) if t["timed"]]  # (async: one in four)
+    sc = sum(t["scan_ms"] for t in tims) / max(1, len(tims))
     print(f"sync {ts * 1e3:.4f} ms/step ({n / ts / 2**30:.0f} GiB/s)   async {ta * 1e3:.4f} ms/step "
           f"({n / ta / 2**30:.0f} GiB/s)   fused scan launch {sc:.4f} ms   chunks {int(fa[-1])}", flush=True)
 import oracle  # noqa: E402
