@@ -2136,6 +2136,10 @@ __host__ __device__ __forceinline__ uint32_t rabin_group_log2(const StreamTable 
     const uint32_t k = st.span_log2 - wp.piece_log2;
     return k < CDC_RABIN_GROUP_LOG2 ? k : CDC_RABIN_GROUP_LOG2;
 }
+// (Its input loads re-fetch: FETCH_SIZE 1.76x of the input, the halves of a
+// 128-byte line being asked for one iteration apart by 1024 lanes per CU.
+// Non-temporal second halves made it 1.90x and the pass slower, and a whole
+// line per iteration needs 169 VGPRs: profiles/r05/r05y_*.)
 constexpr int kRabinReps = CDC_RABIN_REPS;
 constexpr int kRabinWaves = CDC_RABIN_WAVES;  // pieces per block (64 KiB of tables shared by 8 waves)
 
@@ -2228,6 +2232,13 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
             c1 = c2;
             c2 = cur;
         }
+        auto emit = [&](uint64_t a, uint32_t b0, uint32_t b1) {
+            const uint64_t hits = ~(((uint64_t)b1 << 32) | b0);  // bit set = window hit
+            const uint32_t wi = (uint32_t)((a - p0) >> 6);
+            out[wi] = hits;
+            qm |= (uint32_t)(hits == 0) << wi;
+            qa |= (uint32_t)(hits == ~0ull) << wi;
+        };
         uint4 n0 = load16_guarded(base, p0, len), n1 = load16_guarded(base, p0 + 16, len);
         uint4 n2 = load16_guarded(base, p0 + 32, len), n3 = load16_guarded(base, p0 + 48, len);
         for (uint64_t a = p0; a < p1; a += 64) {
@@ -2246,10 +2257,7 @@ __global__ __launch_bounds__(64 * kRabinWaves) void rbits_kernel(const StreamTab
             c0 = q1;
             c1 = q2;
             c2 = q3;
-            const uint64_t hits = ~(((uint64_t)b1 << 32) | b0);  // bit set = window hit
-            out[(a - p0) >> 6] = hits;
-            qm |= (uint32_t)(hits == 0) << ((a - p0) >> 6);
-            qa |= (uint32_t)(hits == ~0ull) << ((a - p0) >> 6);
+            emit(a, b0, b1);
         }
     }
     if (wp.rsum && (w >> 6) >= 8) {  // nw >= 8 words per lane: nw / 8 whole summary bytes per kind
