@@ -1307,7 +1307,7 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     bool settled = false, quiet_stop = false, queued = false;
     uint32_t launched = 0, last_round = 0;
     while (launched < R && !settled) {
-        const uint32_t grp = launched == 0 ? 1u : kGroup;
+        const uint32_t grp = launched == 0 ? walk::kFirstGroupRounds : kGroup;
         const uint32_t end = launched + grp < R ? launched + grp : R;
         for (uint32_t r = launched; r < end; ++r) {
             // Plain Jacobi for the first ahead_after_ rounds, then run-ahead
@@ -1341,12 +1341,12 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         // Later rounds of the group returned at once on the device (the same
         // rule, walk.hip round_stops).
         for (uint32_t r = 0; r < launched; ++r) {
-            const uint64_t ch = h_rf[4 * r], q = h_rf[4 * r + 3] >> 32;
-            if (ch == 0) {
+            const int v = walk::round_verdict(h_rf[4 * r], h_rf[4 * r + 3] >> 32);  // (walk.hpp: shared rule)
+            if (v == walk::kRoundSettled) {
                 settled = true;
                 break;
             }
-            if (2 * q >= ch) {
+            if (v == walk::kRoundQuiet) {
                 last_round = r;
                 quiet_stop = true;
                 break;
@@ -1372,7 +1372,10 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         HIP_TRY(walk::launch_serial(st, wp_, wst_, s));
     }
     (void)lap("fixup");
-    if (!(queued && settled && launched == 1)) {  // (else the gated output already ran)
+    // The gated output queued after the first group ran on the device exactly
+    // when that group settled by the same rule (emit_skips), i.e. when the
+    // loop stopped after it: launched == kFirstGroupRounds.
+    if (!(queued && settled && launched == walk::kFirstGroupRounds)) {  // (else the gated output already ran)
         HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
         HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));

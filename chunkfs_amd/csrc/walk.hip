@@ -667,7 +667,7 @@ __global__ __launch_bounds__(kWalkBlock) void walk_kernel(const StreamTable st, 
 // a quiet-dominated stream to the in-order pass; WalkState::flags[3] counts,
 // in its high half, the chains of flags[0] whose changed exit was a quiet run).
 __device__ __forceinline__ bool round_stops(const unsigned long long *gate) {
-    return gate && (gate[0] == 0 || 2 * (gate[3] >> 32) >= gate[0]);
+    return gate && round_verdict(gate[0], gate[3] >> 32) != kRoundGoOn;
 }
 
 template <int kAlgo, bool kBits>
@@ -2559,9 +2559,9 @@ __device__ __forceinline__ uint64_t block_exclusive(uint64_t v, uint64_t *sh, ui
 __device__ __forceinline__ bool emit_skips(const unsigned long long *egate, uint32_t egn) {
     if (!egate) return false;
     for (uint32_t r = 0; r < egn; ++r) {
-        const unsigned long long ch = egate[4 * r], q = egate[4 * r + 3] >> 32;
-        if (ch == 0) return false;
-        if (2 * q >= ch) return true;
+        const int v = round_verdict(egate[4 * r], egate[4 * r + 3] >> 32);
+        if (v == kRoundSettled) return false;
+        if (v == kRoundQuiet) return true;
     }
     return true;
 }

@@ -20,6 +20,21 @@
 namespace cdc {
 namespace walk {
 
+// Verdict of one fix-up round from its flag block: ch = chains whose exit
+// changed, q = those of them whose changed exit was a quiet-run re-walk.
+// Settled: nothing changed.  Quiet: mostly quiet runs -- chains there keep
+// their phase and each round moves the true one a single segment, so the
+// in-order pass takes over.  One rule for the host's round loop
+// (Engine::run_walk), the device's round gate (round_stops) and the gated
+// output after the first group (emit_skips).
+enum : int { kRoundSettled = 0, kRoundQuiet = 1, kRoundGoOn = 2 };
+__host__ __device__ __forceinline__ int round_verdict(unsigned long long ch, unsigned long long q) {
+    return ch == 0 ? kRoundSettled : (2 * q >= ch ? kRoundQuiet : kRoundGoOn);
+}
+// Rounds in the first group of fix-up launches, behind which the output is
+// queued and gated on the device (Engine::run_walk; emit_skips).
+constexpr unsigned kFirstGroupRounds = 1;
+
 struct WalkParams {
     uint32_t algo;            // cdc_algo_t: 2 rabin, 4 ultra, 5 leap, 6 seq
     uint32_t min, avg, max;
