@@ -264,3 +264,17 @@ def test_chunk_data_two_handles_two_threads():
     assert small == 40 and fb <= small
     for h in chs:
         h.close()
+
+
+def test_host_placement_off_is_exact(monkeypatch):
+    """CHUNKFS_AMD_COPY_NUMA=0 (the A/B path): no placement, unpinned helpers
+    (their own pool), same chunks."""
+    import chunkfs_amd as c
+    monkeypatch.setenv("CHUNKFS_AMD_COPY_NUMA", "0")
+    ch = _chunker("fast")
+    p = c.host_placement(ch)
+    assert p["numa_placement"] is False and p["helpers_pinned"] == 0
+    for n in ((1 << 20) + 5, (6 << 20) + 77, 40 << 20):  # small kernel, ring upload, pageable copy
+        data = oracle.splitmix64_bytes(n, 90 + n % 7)
+        assert (ch.chunk_array(data)[:, 1] == _whole("fast", data)).all(), n
+    ch.close()
