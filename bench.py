@@ -190,7 +190,12 @@ class DeviceEngine:
         events one in four (CHUNKFS_AMD_EVENT_EVERY; an event costs the stream
         ~4 us): the timed steps' sampled batches."""
         allt = [self.ch.timing_back(b) for b in range(min(k, 64) - 1, -1, -1)]
-        return [t for t in allt if t["total_ms"] > 0] or allt
+        return [t for t in allt if t["timed"]]  # (may be empty: callers report the timing as unavailable)
+
+    def sync_step(self, w):
+        """One synchronous batch (cdc_chunk_batch_device): submit, wait, first[]
+        filled on return -- the single-batch latency, nothing pipelined."""
+        return self.ch.chunk_batch_device(w.ptrs_a, w.lens_a, w.out.data_ptr(), w.cap)
 
     def sync(self):
         self.ch.batch_sync()
@@ -226,7 +231,11 @@ class StubEngine:
         return first
 
     def timing(self):
-        return {"scan_ms": 0.0, "total_ms": 0.0, "resolve_ms": 0.0, "fixup_iterations": 0, "walk_fallback_steps": 0}
+        return {"scan_ms": 0.0, "total_ms": 0.0, "resolve_ms": 0.0, "fixup_iterations": 0, "walk_fallback_steps": 0,
+                "timed": 1}
+
+    def sync_step(self, w):
+        return self.step(w)
 
     def timings(self, k):
         return [self.timing() for _ in range(min(k, 64))]
@@ -278,6 +287,38 @@ def timed_steps(eng, w, steps, warmup, world, red_dev, settle_ms=0.0):
     return el, first, tims
 
 
+def latency_leg(eng, w, reps=20):
+    """Synchronous single-batch latency of the headline workload: one
+    cdc_chunk_batch_device call (tables, scan, resolve, host wait; nothing
+    pipelined), wall time per call, beside the pipelined `value`."""
+    eng.sync()
+    for _ in range(3):
+        eng.sync_step(w)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        eng.sync_step(w)
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    t = eng.timing()
+    return {"definition": "one synchronous cdc_chunk_batch_device call on the headline stream(s), wall time",
+            "calls": reps, "median_ms": ts[len(ts) // 2] * 1e3, "min_ms": ts[0] * 1e3,
+            "GiBps_at_median": sum(w.lens) / ts[len(ts) // 2] / (1 << 30),
+            "last_call_scan_ms": t["scan_ms"], "last_call_resolve_ms": t["resolve_ms"]}
+
+
+def sustained_leg(eng, w, ms_per_step, target_ms=150.0):
+    """The headline workload timed over >= target_ms of back-to-back steps
+    (the headline's 100 steps are ~28 ms): shows whether clocks or power droop
+    under sustained load."""
+    steps = max(200, int(target_ms / max(ms_per_step, 1e-3)) + 1)
+    el, _, tims = timed_steps(eng, w, steps, 5, 1, None)
+    scan = sum(t["scan_ms"] for t in tims) / len(tims) if tims else None
+    return {"steps": steps, "timed_ms": el * 1e3, "ms_per_step": el / steps * 1e3,
+            "GiBps": sum(w.lens) * steps / el / (1 << 30), "scan_ms": scan,
+            "scan_batches_timed": len(tims)}
+
+
 def config4_leg(args, eng, rank, world, red_dev):
     """Config 4 (BASELINE configs[3]): 1024 x 64 MiB streams split across the
     ranks (strong scaling, no data-path collective); at N > 1 rank 0 also times
@@ -290,13 +331,13 @@ def config4_leg(args, eng, rank, world, red_dev):
     _settle()
     el, first, tims = timed_steps(eng, w, steps, 2, world, red_dev)
     total = sharding.sum_over_ranks(sum(shard.lens), red_dev) * steps
-    scan = sum(t["scan_ms"] for t in tims) / len(tims)
+    scan = sum(t["scan_ms"] for t in tims) / len(tims) if tims else 0.0
     out = {"workload": f"config4: {args.batch_streams} x {args.batch_stream_bytes} B streams split across "
                        f"{world} GPU(s)", "scaling": "strong", "steps": steps,
            "value": sharding.aggregate_gibps(total, el), "unit": "GiB/s", "ms_per_step": el / steps * 1e3,
            "streams_per_gpu": len(shard.lens), "bytes_per_gpu": sum(shard.lens),
            "chunks_total": sharding.sum_over_ranks(int(first[-1]) if first is not None else 0, red_dev),
-           "scan_ms": scan,
+           "scan_ms": scan if tims else None,  # (None: no timed batch among the steps)
            "scan_frac_of_hbm": (sum(shard.lens) / (scan * 1e-3) / 1e9 / HBM_PEAK_GBS) if scan > 0 else None}
     if not args.no_parity and not args.stub and rank == 0 and len(shard.lens):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -723,15 +764,27 @@ def config3_line(args, local, base_bytes=256 << 20, versions=16):
     out = torch.empty((cap, 2), dtype=torch.int64, device=dev)
     dig = torch.empty((cap, 32), dtype=torch.uint8, device=dev)
 
+    ptrs = [b.data_ptr() for b in bufs]
+    ix = cfa.DedupIndex(cap + 64, device=local)  # (sized once; cleared per pass: Database::clear)
+    phase = {}
+
     def gpu_pass():
-        first = ch.chunk_batch_device([b.data_ptr() for b in bufs], lens, out.data_ptr(), cap)
-        ix = cfa.DedupIndex(int(first[-1]) + 64, device=local)
-        for i, b in enumerate(bufs):
-            a, z = int(first[i]), int(first[i + 1])
-            ch.sha256_chunks_device(b.data_ptr(), out[a:].data_ptr(), z - a, dig[a:].data_ptr())
-            ix.insert_device(dig[a:].data_ptr(), out[a:].data_ptr(), z - a)
+        # one launch per stage over all versions: chunk every file, hash every
+        # chunk (cdc_sha256_batch_device), insert every digest in file order
+        # (the reference's sequential writes: first insert wins)
+        ix.clear()
+        t0 = time.perf_counter()
+        first = ch.chunk_batch_device(ptrs, lens, out.data_ptr(), cap)
+        t1 = time.perf_counter()
+        ch.sha256_batch_device(ptrs, first, out.data_ptr(), dig.data_ptr())
+        t2 = time.perf_counter()
+        ix.insert_device(dig.data_ptr(), out.data_ptr(), int(first[-1]))
+        st = ix.stats()
         torch.cuda.synchronize()
-        return first, ix.stats()
+        t3 = time.perf_counter()
+        phase.update(chunk_ms=(t1 - t0) * 1e3, sha256_ms=(t2 - t1) * 1e3, index_ms=(t3 - t2) * 1e3,
+                     sha256_kernel_ms=ch.last_timing()["hash_ms"])
+        return first, st
 
     gpu_pass()
     _settle()
@@ -751,6 +804,7 @@ def config3_line(args, local, base_bytes=256 << 20, versions=16):
     t_cpu = time.perf_counter() - t0
     cpu_ratio = written / sum(db.values())
     ch.close()
+    del ix
     return {"workload": f"config3 substitute: {versions} versions of a {base_bytes} B splitmix64 base, "
                         "~1 % seeded overwrites/inserts/deletes per version (gcc tarball unavailable offline)",
             "algo": "RabinCDC (parity unpinned)", "sizes": list(sizes), "bytes": int(total),
@@ -759,6 +813,8 @@ def config3_line(args, local, base_bytes=256 << 20, versions=16):
             "chunks_bit_exact": parity, "unique_chunks": st["unique_chunks"],
             "gpu_GiBps": total / t_gpu / (1 << 30),
             "gpu_definition": "device-resident: Rabin chunking + SHA-256 per chunk + dedup index inserts, wall time",
+            "gpu_phase_ms": phase,
+            "sha256_GiBps": total / (phase["sha256_kernel_ms"] * 1e-3) / (1 << 30) if phase.get("sha256_kernel_ms") else None,
             "cpu_GiBps": total / t_cpu / (1 << 30),
             "cpu_definition": "oracle Rabin (C) + hashlib SHA-256 + dict, single thread"}
 
@@ -876,6 +932,7 @@ def summary(line, read_gbs):
     """The line's headline figures in one small object (printed last)."""
     g = lambda *ks: _dig(line, ks)  # noqa: E731
     out = {"value_GiBps": line.get("value"), "ms_per_step": line.get("ms_per_step"),
+           "sustained_ms_per_step": g("sustained", "ms_per_step"), "sync_latency_ms": g("latency_sync", "median_ms"),
            "parity_vs_oracle": line.get("parity_vs_oracle"),
            "scan_frac_of_hbm": g("roofline", "frac"), "scan_frac_of_achievable": g("roofline", "frac_of_achievable"),
            "achievable_read_GBps": read_gbs, "end_to_end_frac_of_hbm": g("roofline", "end_to_end", "frac"),
@@ -963,6 +1020,7 @@ def main(argv=None):
     read_gbs, read_ms = eng.read_bw(w) if shard.lens and shard.lens[0] else (None, None)
     total_bytes = sharding.sum_over_ranks(bytes_rank, red_dev) * args.steps
     value = sharding.aggregate_gibps(total_bytes, elapsed)
+    tims = tims or [dict(scan_ms=0.0, total_ms=0.0, resolve_ms=0.0, fixup_iterations=0, timed=0)]  # (none timed)
     scan_avg_ms = sum(t["scan_ms"] for t in tims) / len(tims)
     nchunks = int(first[-1])
     total_chunks = sharding.sum_over_ranks(nchunks, red_dev)
@@ -971,6 +1029,9 @@ def main(argv=None):
     e2e = bytes_rank / (ms_per_step * 1e-3) / 1e9  # per-GPU bytes / wall step time
 
     extras = {}
+    if rank == 0 and world == 1 and not args.stub and shard.lens and shard.lens[0]:
+        extras["sustained"] = sustained_leg(eng, w, ms_per_step)
+        extras["latency_sync"] = latency_leg(eng, w)
     if rank == 0 and world == 1 and not args.stub:
         if args.hash and shard.lens[0]:
             n0 = int(first[1]) - int(first[0])

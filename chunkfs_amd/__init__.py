@@ -127,6 +127,7 @@ class Chunker:
         out = np.empty((max(cap, 1), 2), dtype=np.uint64)
         cnt = check(lib().cdc_chunk_data(self._h, ptr, n,
                                          out.ctypes.data_as(ctypes.POINTER(cdc_chunk_t)), cap))
+        self._drained()
         del keep
         assert cnt <= cap
         return out[:cnt]
@@ -142,6 +143,7 @@ class Chunker:
         cnt = check(lib().cdc_chunk_and_hash(self._h, ptr, n,
                                              out.ctypes.data_as(ctypes.POINTER(cdc_chunk_t)),
                                              dig.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), cap))
+        self._drained()
         del keep
         assert cnt <= cap
         return out[:cnt], dig[:cnt]
@@ -151,6 +153,19 @@ class Chunker:
         check(lib().cdc_sha256_chunks_device(self._h, ctypes.c_void_p(d_data), ctypes.c_void_p(d_chunks),
                                              n_chunks, ctypes.c_void_p(d_digests),
                                              None if stream is None else ctypes.c_void_p(stream)))
+
+    def sha256_batch_device(self, d_ptrs, first, d_chunks, d_digests, stream=None):
+        """SHA-256 of every chunk of a multi-stream batch in one launch
+        (cdc_sha256_batch_device): stream i's chunks are d_chunks[first[i] ..
+        first[i+1]), offsets relative to d_ptrs[i]."""
+        ptrs = np.ascontiguousarray(np.asarray(d_ptrs, dtype=np.uint64))
+        fa = np.ascontiguousarray(np.asarray(first, dtype=np.uint64))
+        assert fa.size == ptrs.size + 1
+        check(lib().cdc_sha256_batch_device(self._h, int(ptrs.size), ctypes.c_void_p(ptrs.ctypes.data),
+                                            ctypes.c_void_p(fa.ctypes.data), ctypes.c_void_p(int(d_chunks)),
+                                            ctypes.c_void_p(int(d_digests)),
+                                            None if stream is None else ctypes.c_void_p(stream)))
+        self._drained()
 
     def chunk_data(self, data, empty=None):
         """Chunker::chunk_data (src/lib.rs:80): chunks tiling `data`, appended to `empty`."""
@@ -186,6 +201,7 @@ class Chunker:
                                            ctypes.c_void_p(lens_a.ctypes.data), ctypes.c_void_p(int(d_out_ptr)),
                                            out_cap, ctypes.c_void_p(first.ctypes.data),
                                            ctypes.c_void_p(int(stream))))
+        self._drained()
         return first
 
     def chunk_batch_device_async(self, d_ptrs, lens, d_out_ptr, out_cap, stream=0):
@@ -196,17 +212,26 @@ class Chunker:
         lens_a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
         n = int(lens_a.size)
         first = np.zeros(n + 1, dtype=np.uint64)
-        self.__dict__.setdefault("_pending", []).append(first)  # the library writes it at batch_sync()
+        pend = self.__dict__.setdefault("_pending", [])
+        pend.append(first)  # the library writes it when the batch is collected
         check(lib().cdc_chunk_batch_device_async(self._h, n, ctypes.c_void_p(ptrs.ctypes.data),
                                                  ctypes.c_void_p(lens_a.ctypes.data),
                                                  ctypes.c_void_p(int(d_out_ptr)), out_cap,
                                                  ctypes.c_void_p(first.ctypes.data), ctypes.c_void_p(int(stream))))
+        # At most 3 batches are in flight (a submit collects the batch 3 before
+        # it), so older arrays are already written: keep only those 3.
+        del pend[:-3]
         return first
+
+    def _drained(self):
+        """Every library call but an async submit completes the batches in
+        flight first (include/chunkfs_amd.h): their first[] arrays are written."""
+        self.__dict__["_pending"] = []
 
     def batch_sync(self):
         """cdc_batch_sync: complete every enqueued batch; the last one's chunk count."""
         r = check(lib().cdc_batch_sync(self._h))
-        self._pending = []
+        self._drained()
         return r
 
     def batch_max_chunks(self, lens):
@@ -217,6 +242,7 @@ class Chunker:
     def last_timing(self):
         t = cdc_timing_t()
         check(lib().cdc_last_timing(self._h, ctypes.byref(t), ctypes.sizeof(t)))
+        self._drained()
         return {f: getattr(t, f) for f, _ in cdc_timing_t._fields_}
 
     def timing_back(self, back):

@@ -25,7 +25,7 @@ EXPORTS = [
     "cdc_chunk_batch_device", "cdc_chunk_batch_device_async", "cdc_batch_sync", "cdc_batch_max_chunks",
     "cdc_last_timing",
     "cdc_fs_write", "cdc_write_begin", "cdc_write_segment", "cdc_write_drain", "cdc_write_finish",
-    "cdc_sha256_chunks_device", "cdc_chunk_and_hash",
+    "cdc_sha256_chunks_device", "cdc_sha256_batch_device", "cdc_chunk_and_hash",
     "cdc_index_create", "cdc_index_destroy", "cdc_index_clear", "cdc_index_insert_device",
     "cdc_index_stats",
     "cdc_fill_splitmix64_device", "cdc_version", "cdc_abi_version",
@@ -144,6 +144,8 @@ def lib():
     L.cdc_debug_timing_back.restype = ctypes.c_int
     L.cdc_sha256_chunks_device.argtypes = [P, P, P, sz, P, P]
     L.cdc_sha256_chunks_device.restype = ctypes.c_int
+    L.cdc_sha256_batch_device.argtypes = [P, sz, P, P, P, P, P]
+    L.cdc_sha256_batch_device.restype = ctypes.c_int
     L.cdc_chunk_and_hash.argtypes = [P, P, sz, ctypes.POINTER(cdc_chunk_t), u8p, sz]
     L.cdc_chunk_and_hash.restype = ctypes.c_int64
     L.cdc_index_create.argtypes = [ctypes.c_int, sz, ctypes.POINTER(P)]

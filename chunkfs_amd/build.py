@@ -11,7 +11,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libchunkfs_amd.so")
-SOURCES = ["fastcdc.hip", "small.hip", "walk.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "hostpath.cpp", "capi.cpp",
+SOURCES = ["fastcdc.hip", "fastcdc_ovl.hip", "small.hip", "walk.hip", "util_kernels.hip", "sha256.hip", "index.hip", "engine.cpp", "hostpath.cpp", "capi.cpp",
            "index_host.cpp"]
 HEADERS = ["fastcdc.hpp", "small.hpp", "walk.hpp", "cdc_kernels.hpp", "sha256.hpp", "index.hpp", "engine.hpp"]
 ARCH = "gfx950"
@@ -62,7 +62,8 @@ def build(force=False, defines=(), lib=None, build_dir=None):
         s = os.path.join(CSRC, src)
         o = os.path.join(bdir, src + ".o")
         objs.append(o)
-        if force or _newer(o, [s] + common):
+        deps = [s] + common + ([os.path.join(CSRC, "fastcdc.hip")] if src == "fastcdc_ovl.hip" else [])
+        if force or _newer(o, deps):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
             _run([HIPCC] + CFLAGS + [f"-D{d}" for d in defines] + lang + ["-c", s, "-o", o])
     if force or _newer(out_lib, objs):

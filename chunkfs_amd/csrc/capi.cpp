@@ -184,6 +184,14 @@ int cdc_sha256_chunks_device(cdc_handle_t *h, const uint8_t *d_data,
                                     static_cast<hipStream_t>(hip_stream));
 }
 
+int cdc_sha256_batch_device(cdc_handle_t *h, size_t n_streams, const uint8_t *const *d_streams,
+                            const uint64_t *first, const cdc_chunk_t *d_chunks, uint8_t *d_digests,
+                            void *hip_stream) {
+    if (!h) return (int)bad_handle();
+    return h->engine->sha256_batch(n_streams, d_streams, first, d_chunks, d_digests,
+                                   static_cast<hipStream_t>(hip_stream));
+}
+
 int64_t cdc_chunk_and_hash(cdc_handle_t *h, const uint8_t *data, size_t len,
                            cdc_chunk_t *out, uint8_t *digests, size_t cap) {
     if (!h) return bad_handle();
@@ -222,7 +230,7 @@ int64_t cdc_debug_copy(cdc_handle_t *h, int what, void *out, size_t max_bytes) {
     return h->engine->debug_copy(what, out, max_bytes);
 }
 
-const char *cdc_version(void) { return "chunkfs_amd 0.5 gfx950 abi 3"; }
+const char *cdc_version(void) { return "chunkfs_amd 0.6 gfx950 abi 4"; }
 
 uint32_t cdc_abi_version(void) { return CHUNKFS_AMD_ABI_VERSION; }
 

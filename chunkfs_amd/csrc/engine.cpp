@@ -113,6 +113,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         fp.mask_l_sh = fp.mask_l << fp.tshift;
         if (const char *d = std::getenv("CHUNKFS_AMD_DIAG")) fp.diag = (uint32_t)std::atoi(d);
         if (const char *v = std::getenv("CHUNKFS_AMD_EVENT_EVERY")) e->event_every_ = std::max(1, std::atoi(v));
+        if (const char *v = std::getenv("CHUNKFS_AMD_OVERLAP")) e->ovl_on_ = std::atoi(v) != 0;  // (A/B, default off)
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
         e->small_span_log2_ = l2 > 14 ? l2 : 14;
@@ -128,6 +129,10 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         if (cap > 256) cap = 256;
         e->cap_ = (uint32_t)cap;
         e->smax_ = (uint32_t)(span / ((min / 2) * 2) + 2);
+        // The overlap set's resolve windows hold 384 records (11 spans): keep
+        // it to sizes whose windows expect <= 256 (avg >= 8 KiB at max <= 64
+        // KiB); denser records would send windows to the slow global path.
+        if (11 * (span >> (pc < 63 ? pc : 63)) > 256) e->ovl_on_ = false;
         // Small-stream path (small.hip): its per-lane and per-block record
         // budgets assume sparse hits, ~2^-10 per position or rarer.
         const uint32_t pmin = (uint32_t)std::min(__builtin_popcountll(fp.mask_s), __builtin_popcountll(fp.mask_l));
@@ -192,12 +197,15 @@ Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
     if (fb_any_) (void)fast_drain();
     if (own_stream_) (void)hipStreamSynchronize(own_stream_);
+    if (res_stream_) (void)hipStreamSynchronize(res_stream_);
     (void)hipFree(ws_);
     (void)hipFree(small_mem_);
     (void)hipFree(d_gear_);
     (void)hipFree(d_data_);
     (void)hipFree(d_out_);
     (void)hipFree(d_dig_);
+    (void)hipFree(d_sha_tab_);
+    (void)hipHostFree(h_sha_tab_);
     (void)hipFree(d_counter_);
     (void)hipFree(d_wtabs_);
     (void)hipFree(wws_);
@@ -218,6 +226,10 @@ Engine::~Engine() {
         for (auto &ev : slot)
             if (ev) (void)hipEventDestroy(ev);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
+    for (auto &ev : scan_ev_)
+        if (ev) (void)hipEventDestroy(ev);
+    if (res_ev_) (void)hipEventDestroy(res_ev_);
+    if (res_stream_) (void)hipStreamDestroy(res_stream_);
 }
 
 int Engine::set_gear(const uint64_t *gear) {
@@ -226,7 +238,7 @@ int Engine::set_gear(const uint64_t *gear) {
         return CDC_EINVAL;
     }
     if (fb_any_) {  // the batches in flight finish with the table they were submitted with
-        const int64_t r = fast_drain();
+        const int64_t r = drain_implicit();
         if (r < 0) return (int)r;
     }
     if (wr_.active) {  // windows already chunked used the old table: a write never mixes two
@@ -300,7 +312,7 @@ int Engine::ensure_workspace(uint64_t spans, size_t n) {
     }
     const size_t o_starts = take(S * smax * 8);  // chunk starts beyond the LDS-resident ones
     const size_t o_first = take((N + 1) * 8);
-    const uint64_t nb = p3::resolve_blocks(S) + 2;
+    const uint64_t nb = std::max(p3::resolve_blocks(S), p3::ovl::resolve_blocks(S)) + 2;
     const size_t o_desc = take(6 * nb * 8);
     (void)hipFree(ws_);
     ws_ = nullptr;
@@ -353,7 +365,26 @@ int64_t Engine::chunk_batch_device_async(size_t n, const uint8_t *const *d_strea
 
 int64_t Engine::batch_sync() {
     HIP_TRY(hipSetDevice(device_));
-    return fast_drain();
+    if (fb_any_) {
+        held_valid_ = false;
+        return fast_drain();
+    }
+    if (held_valid_) {  // an implicit drain already completed them: its result
+        held_valid_ = false;
+        return held_;
+    }
+    return 0;
+}
+
+// A drain that another call makes on the caller's behalf (any call on the
+// handle completes the async batches first): its result -- the last batch's
+// chunk count, or the error of a failed collection -- is what the next
+// cdc_batch_sync returns.
+int64_t Engine::drain_implicit() {
+    if (!fb_any_) return 0;
+    held_ = fast_drain();
+    held_valid_ = true;
+    return held_;
 }
 
 int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
@@ -391,7 +422,7 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
     // completion here, after the batches in flight.
     const bool pipe = algo_ == CDC_ALGO_FASTCDC && n > 0 && bytes > kSmallBatch;
     if (!pipe && fb_any_) {
-        const int64_t r = fast_drain();
+        const int64_t r = drain_implicit();
         if (r < 0) return r;
     }
     if (pipe) {
@@ -399,7 +430,7 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
         // reads are recorded on every event_every_-th batch only -- each
         // event costs the stream ~4 us, r05t)
         const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s,
-                                      !async || fb_seq_ % event_every_ == 0);
+                                      !async || fb_seq_ % event_every_ == 0, async && ovl_on_);
         if (r < 0 || async) return r;
         return fast_drain();
     }
@@ -426,7 +457,7 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
         // (kSmallFallback: the regular pipeline below)
     }
     if (algo_ == CDC_ALGO_FASTCDC) {  // small batches: one scan + resolve, waited for here
-        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s, true);
+        const int64_t r = fast_submit(n, d_streams, lens, d_out, out_cap, first, bytes, s, true, false);
         if (r < 0) return r;
         return fast_drain();
     }
@@ -480,10 +511,15 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
 // the resolve launches; no host wait.  The host collects it (fast_collect)
 // when its stats block is needed again or at fast_drain().
 int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
-                            size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s, bool timed) {
-    if (fb_any_ && s != fb_stream_) {  // one pipeline per stream
-        const int64_t r = fast_drain();
+                            size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s, bool timed, bool ovl) {
+    if (fb_any_ && (s != fb_stream_ || ovl != fb_ovl_)) {  // one pipeline per stream (and kernel set)
+        const int64_t r = drain_implicit();
         if (r < 0) return r;
+    }
+    if (ovl && !res_stream_) {
+        HIP_TRY(hipStreamCreateWithFlags(&res_stream_, hipStreamNonBlocking));
+        for (auto &ev : scan_ev_) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&res_ev_, hipEventDisableTiming));
     }
     const uint32_t sl2 = bytes <= kSmallBatch ? small_span_log2_ : span_log2_;
     uint64_t spans = 0;
@@ -491,7 +527,7 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     const bool zero_copy = bytes <= kSmallBatch && n <= kZeroCopyStreams;
     const bool grow = !(h_stage_ && h_stage_streams_ >= n) || !(ws_ && spans <= ws_spans_ && n <= ws_streams_);
     if (fb_any_ && (zero_copy || grow)) {  // (buffers the batches in flight use)
-        const int64_t r = fast_drain();
+        const int64_t r = drain_implicit();
         if (r < 0) return r;
     }
     const uint64_t seq = fb_seq_;
@@ -560,9 +596,9 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     p3::Resolve rs = rs3_;
     rs.gen = ++res_gen_;
     FastBatch &rec = fb_[seq % 3];
-    rec = FastBatch{};
-    rec.live = true;
+    rec = FastBatch{};  // (live only once every launch is enqueued, below)
     rec.resolved = true;
+    rec.ovl = ovl;
     rec.slot = slot;
     rec.h = hb;
     rec.n = n;
@@ -574,16 +610,35 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
     tev_timed_[seq % kTimeRing] = timed;
     rec.timed = timed;
     if (timed) HIP_TRY(hipEventRecord(ev[0], s));
-    if (spans)
-        HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails, num_cus_,
-                                s));
-    if (timed) HIP_TRY(hipEventRecord(ev[1], s));
-    if (spans) HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, s));
-    if (timed) HIP_TRY(hipEventRecord(ev[2], s));
+    if (!ovl) {
+        if (spans)
+            HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails,
+                                    num_cus_, s));
+        if (timed) HIP_TRY(hipEventRecord(ev[1], s));
+        if (spans) HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, s));
+        if (timed) HIP_TRY(hipEventRecord(ev[2], s));
+    } else {
+        // The resolve goes to the second stream behind this scan's event, so
+        // it runs beside the NEXT batch's scan (the overlap set fits one
+        // resolve block next to each CU's scan block).  Resolves stay in order
+        // on that stream (the look-back descriptors and the spilled chunk
+        // starts are shared).  No wait guards the device slot: its previous
+        // user, batch seq - kSlots, is complete -- batch seq - kHostSlots was
+        // collected above (or by a drain), and resolves retire in order.
+        static_assert(kSlots > kHostSlots, "device slots must outlast the host blocks");
+        if (spans) HIP_TRY(p3::ovl::launch_scan(st, fp_, d_gear_, f.cand, cp, f.d_tails, f.n_tails, num_cus_, s));
+        if (timed) HIP_TRY(hipEventRecord(ev[1], s));
+        HIP_TRY(hipEventRecord(scan_ev_[slot], s));
+        HIP_TRY(hipStreamWaitEvent(res_stream_, scan_ev_[slot], 0));
+        if (spans) HIP_TRY(p3::ovl::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, res_stream_));
+        if (timed) HIP_TRY(hipEventRecord(ev[2], res_stream_));
+    }
+    rec.live = true;
     fb_seq_ = seq + 1;
     fast_batches_ = fb_seq_;
     fb_any_ = true;
     fb_stream_ = s;
+    fb_ovl_ = ovl;
     cand_ = f.cand;
     last_spans_ = spans;
     return 0;
@@ -603,6 +658,13 @@ int64_t Engine::fast_drain() {
         b.live = false;
         if (r && !rc) rc = r;
         if (q == last && !rc) total = (int64_t)b.first[b.n];
+    }
+    if (fb_ovl_) {
+        // later work on the caller's stream is ordered after the resolves
+        if (!rc && hipEventRecord(res_ev_, res_stream_) == hipSuccess)
+            (void)hipStreamWaitEvent(fb_stream_, res_ev_, 0);
+        else
+            (void)hipStreamSynchronize(res_stream_);
     }
     if (rc) (void)hipStreamSynchronize(fb_stream_);  // (nothing of a failed pipeline stays in flight)
     fb_any_ = false;
@@ -628,7 +690,7 @@ int Engine::fast_collect(int k) {
     }
     if (h_misc[p3::kStatDone] == ~0ull) {  // (slow batch or a failure: wait for the stream itself)
         if (b.timed) HIP_TRY(hipEventSynchronize(tev_[b.seq % kTimeRing][2]));
-        else HIP_TRY(hipStreamSynchronize(fb_stream_));
+        else HIP_TRY(hipStreamSynchronize(b.ovl ? res_stream_ : fb_stream_));
     }
     b.live = false;
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
@@ -639,13 +701,13 @@ int Engine::fast_collect(int k) {
     if (fp_.diag & 64) {  // resolve block spans (100 MHz stamps -> us)
         const uint64_t *d = h_misc + p3::kStatDiag0;
         const uint64_t s0 = ~d[0], s1 = d[1], e1 = d[2], e0 = ~d[3];
-        const double blocks = (double)p3::resolve_blocks(b.spans);
+        const double blocks = (double)(b.ovl ? p3::ovl::resolve_blocks(b.spans) : p3::resolve_blocks(b.spans));
         std::fprintf(stderr, "resolve blocks, us: scan's last block end -> first start %.2f  starts spread %.2f  "
                              "first start -> first end %.2f  -> last end %.2f  longest block %.2f  mean block %.2f\n",
                      ((double)s0 - (double)d[6]) / 100.0, (s1 - s0) / 100.0, (e0 - s0) / 100.0, (e1 - s0) / 100.0,
                      d[4] / 100.0, d[5] / 100.0 / (blocks ? blocks : 1.0));
     } else if (fp_.diag & 128) {
-        const double waves = (double)p3::resolve_blocks(b.spans) * 8;
+        const double waves = b.ovl ? (double)p3::ovl::resolve_blocks(b.spans) * 4 : (double)p3::resolve_blocks(b.spans) * 8;
         std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk "
                              "lookback(w0) out):");
         for (int i = 0; i < p3::kStatDiagN; ++i)
@@ -786,7 +848,7 @@ int Engine::run_small(const uint8_t *data, uint64_t len, cdc_chunk_t *d_out, siz
 // FastCDC batch events: [0] before its scan launch, [1] after it (before the
 // resolve), [2] after the resolve.
 const cdc_timing_t &Engine::timing() {
-    if (fb_any_) (void)fast_drain();
+    if (fb_any_) (void)drain_implicit();  // (a failure is held for the next cdc_batch_sync)
     if (timing_pending_) {
         timing_pending_ = false;
         (void)timing_back((uint32_t)(fast_batches_ - 1 - timing_seq_), timing_);
@@ -795,7 +857,7 @@ const cdc_timing_t &Engine::timing() {
 }
 
 int Engine::timing_back(uint32_t back, cdc_timing_t &out) {
-    if (fb_any_) (void)fast_drain();
+    if (fb_any_) (void)drain_implicit();
     if (algo_ != CDC_ALGO_FASTCDC || back >= kTimeRing || back >= fast_batches_) {
         set_error("cdc_debug_timing_back: no such FastCDC batch in the event ring");
         return CDC_EINVAL;
@@ -871,21 +933,75 @@ int64_t Engine::fs_write(const uint8_t *data, size_t len, size_t seg_size, std::
 
 int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
                           uint8_t *d_digests, hipStream_t s) {
-    if (n && (!d_data || !d_chunks || !d_digests)) {
+    const uint64_t first[2] = {0, n};
+    return sha256_batch(1, &d_data, first, d_chunks, d_digests, s);
+}
+
+// One launch over every chunk of every stream (sha256.hip); the stream table
+// (first[], bases) goes up through a pinned block with one H2D copy.
+int Engine::sha256_batch(size_t n, const uint8_t *const *d_streams, const uint64_t *first,
+                         const cdc_chunk_t *d_chunks, uint8_t *d_digests, hipStream_t s) {
+    if (n == 0) return CDC_OK;
+    if (!d_streams || !first) {
+        set_error("cdc_sha256_batch_device: NULL stream table");
+        return CDC_EINVAL;
+    }
+    if (first[0] != 0) {
+        set_error("cdc_sha256_batch_device: first[0] must be 0");
+        return CDC_EINVAL;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        if (first[i + 1] < first[i]) {
+            set_error("cdc_sha256_batch_device: first[] must be non-decreasing");
+            return CDC_EINVAL;
+        }
+        if (first[i + 1] > first[i] && !d_streams[i]) {
+            set_error("cdc_sha256_batch_device: NULL stream with chunks");
+            return CDC_EINVAL;
+        }
+    }
+    const uint64_t total = first[n];
+    if (total && (!d_chunks || !d_digests)) {
         set_error("cdc_sha256_chunks_device: NULL argument");
         return CDC_EINVAL;
     }
     HIP_TRY(hipSetDevice(device_));
     if (fb_any_) {  // (the chunks it hashes are usually the last batch's)
-        const int64_t r = fast_drain();
+        const int64_t r = drain_implicit();
         if (r < 0) return (int)r;
     }
     hipStream_t st = s ? s : own_stream_;
     (void)timing();  // the last batch's events, before ev_[2] is re-recorded
+    if (total == 0) {
+        timing_.hash_ms = 0;
+        return CDC_OK;
+    }
+    const size_t words = 2 * n + 1;
+    if (sha_tab_cap_ < words) {
+        (void)hipFree(d_sha_tab_);
+        (void)hipHostFree(h_sha_tab_);
+        d_sha_tab_ = h_sha_tab_ = nullptr;
+        sha_tab_cap_ = 0;
+        const size_t want = words + 64;
+        HIP_TRY(hipMalloc(&d_sha_tab_, want * 8));
+        HIP_TRY(hipHostMalloc(&h_sha_tab_, want * 8, hipHostMallocDefault));
+        sha_tab_cap_ = want;
+    }
+    std::memcpy(h_sha_tab_, first, (n + 1) * 8);
+    for (size_t i = 0; i < n; ++i) h_sha_tab_[n + 1 + i] = reinterpret_cast<uint64_t>(d_streams[i]);
+    HIP_TRY(hipMemcpyAsync(d_sha_tab_, h_sha_tab_, words * 8, hipMemcpyHostToDevice, st));
+    ShaBatch b{};
+    b.chunks = reinterpret_cast<const cdc_chunk_pod *>(d_chunks);
+    b.n_chunks = total;
+    b.first = d_sha_tab_;
+    b.base = d_sha_tab_ + n + 1;
+    b.n_streams = (uint32_t)n;
+    b.digests = reinterpret_cast<uint32_t *>(d_digests);
+    b.counter = d_counter_;
     HIP_TRY(hipEventRecord(ev_[3], st));
-    HIP_TRY(launch_sha256(d_data, d_chunks, n, d_digests, d_counter_, num_cus_, st));
+    HIP_TRY(launch_sha256(b, num_cus_, st));
     HIP_TRY(hipEventRecord(ev_[2], st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipStreamSynchronize(st));  // (also: the pinned table may be rewritten by the next call)
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, ev_[3], ev_[2]));
     timing_.hash_ms = ms;
@@ -894,7 +1010,7 @@ int Engine::sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, si
 
 int64_t Engine::debug_copy(int what, void *out, size_t max_bytes) {
     if (fb_any_) {
-        const int64_t r = fast_drain();
+        const int64_t r = drain_implicit();
         if (r < 0) return r;
     }
     if (algo_ != CDC_ALGO_FASTCDC || !ws_) {
@@ -923,7 +1039,7 @@ int64_t Engine::debug_copy(int what, void *out, size_t max_bytes) {
 int Engine::read_bw(const uint8_t *d_buf, size_t len, int reps, double *ms) {
     HIP_TRY(hipSetDevice(device_));
     if (fb_any_) {
-        const int64_t r = fast_drain();
+        const int64_t r = drain_implicit();
         if (r < 0) return (int)r;
     }
     uint64_t *d_acc = nullptr;

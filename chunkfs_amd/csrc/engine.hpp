@@ -109,6 +109,9 @@ class Engine {
     // SHA-256 of chunks of one device-resident stream (Sha256Hasher::hash).
     int sha256_device(const uint8_t *d_data, const cdc_chunk_t *d_chunks, size_t n,
                       uint8_t *d_digests, hipStream_t s);
+    // The same over n streams in one launch (cdc_sha256_batch_device).
+    int sha256_batch(size_t n, const uint8_t *const *d_streams, const uint64_t *first, const cdc_chunk_t *d_chunks,
+                     uint8_t *d_digests, hipStream_t s);
     int64_t chunk_batch_device(size_t n, const uint8_t *const *d_streams,
                                const uint64_t *lens, cdc_chunk_t *d_out,
                                size_t out_cap, uint64_t *first, hipStream_t stream);
@@ -158,10 +161,12 @@ class Engine {
     // batch's results, drain every batch in flight.
     int64_t batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
                          size_t out_cap, uint64_t *first, hipStream_t stream, bool async);
+    // ovl: the overlap kernel set (fastcdc_ovl.hip), the resolve on res_stream_.
     int64_t fast_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
-                        size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s, bool timed);
+                        size_t out_cap, uint64_t *first, uint64_t bytes, hipStream_t s, bool timed, bool ovl);
     int fast_collect(int rec);
     int64_t fast_drain();
+    int64_t drain_implicit();  // fast_drain for another call: its result is kept for batch_sync
     // One small FastCDC stream in one launch (small.hip): CDC_OK, kSmallFallback
     // (a budget was exceeded: run the regular pipeline) or a CDC_E* code.
     static constexpr int kSmallFallback = 1;
@@ -221,13 +226,15 @@ class Engine {
     p3::Resolve rs3_{};            // look-back descriptors (generation-tagged, never re-zeroed)
     uint64_t res_gen_ = 0;
     uint64_t *d_tails_ = nullptr;  // [streams] ragged last span ids (walk engine: unused)
-    // FastCDC batches in flight: device tables and candidates in two slots
-    // (slot = sequence number % 2; stream order protects them) whose uploaded
-    // tables are kept to skip unchanged H2D copies; host staging in three
-    // slots (batch record k % 3, below): batch k's block -- tables going in,
-    // stats ++ first[] coming back -- is read at its collection, before
-    // submit k+3 reuses it.
-    static constexpr int kSlots = 2, kHostSlots = 3;
+    // FastCDC batches in flight: device tables and candidates in four slots
+    // (slot = sequence number % 4) whose uploaded tables are kept to skip
+    // unchanged H2D copies; host staging in three slots (batch record k % 3,
+    // below): batch k's block -- tables going in, stats ++ first[] coming
+    // back -- is read at its collection, before submit k+3 reuses it.  A
+    // device slot outlives its host block, so when batch k is submitted the
+    // slot's previous user k-4 is complete (k-3 was collected): no stream
+    // wait guards it, even with the resolves on a second stream.
+    static constexpr int kSlots = 4, kHostSlots = 3;
     struct FastSlot {
         Candidates cand{};
         const uint8_t **d_ptrs = nullptr;
@@ -240,7 +247,7 @@ class Engine {
     // scan + resolve enqueued at submit, collected (done word, first[]) by the
     // submit three later or by fast_drain.
     struct FastBatch {
-        bool live = false, resolved = false, timed = true;
+        bool live = false, resolved = false, timed = true, ovl = false;
         int slot = 0;                // device slot
         uint64_t *h = nullptr;       // host staging block (slot seq % kHostSlots)
         size_t n = 0;
@@ -253,6 +260,20 @@ class Engine {
     uint64_t fb_seq_ = 0;           // batches submitted
     hipStream_t fb_stream_ = nullptr;  // the stream of the batches in flight
     bool fb_any_ = false;           // a batch is in flight
+    bool fb_ovl_ = false;           // ... of the overlap set (resolves on res_stream_)
+    // Overlapped async batches (CHUNKFS_AMD_OVERLAP=1, where the overlap
+    // set's resolve windows fit): batch k's resolve on res_stream_, behind
+    // scan_ev_[slot k], beside batch k+1's scan; res_ev_ orders the caller's
+    // stream after them at a drain.  Off by default: measured 0.33 vs 0.278
+    // ms per 1 GiB step -- the scan is issue-bound, and the co-resident
+    // resolve slowed it from 0.217 to 0.296 ms while itself taking 0.22 ms
+    // (profiles/r06/r06a_*).
+    bool ovl_on_ = false;
+    hipStream_t res_stream_ = nullptr;
+    hipEvent_t scan_ev_[kSlots] = {};
+    hipEvent_t res_ev_ = nullptr;
+    int64_t held_ = 0;              // result of the last implicit drain (drain_implicit)
+    bool held_valid_ = false;
     const uint64_t *cur_tails_ = nullptr;  // this batch's: d_tails_ or the staging block's
     uint32_t n_tails_ = 0;
     uint64_t *d_first_ = nullptr;  // [n+1] (fixed-size path)
@@ -309,6 +330,8 @@ class Engine {
     uint8_t *d_dig_ = nullptr;               // [d_dig_cap_ * 32] digests (host path)
     size_t d_dig_cap_ = 0;
     unsigned long long *d_counter_ = nullptr;  // SHA-256 work counter
+    uint64_t *d_sha_tab_ = nullptr, *h_sha_tab_ = nullptr;  // SHA-256 batch stream table: first[n+1] ++ bases[n]
+    size_t sha_tab_cap_ = 0;
 
     cdc_timing_t timing_{};
     bool timing_pending_ = false;  // FastCDC events not read yet (see timing())

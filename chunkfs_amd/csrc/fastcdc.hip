@@ -551,11 +551,24 @@ struct ScanLds {
 // hashes it serially from hash 0; its first 48 positions are re-tested at the
 // end with the true carry-in (lane l-1's final hash, one DPP shift; lane 0's
 // from the 48 bytes before the span).  Ragged last spans: scan_tail_kernel.
+#ifndef CDC_SCAN_DYN
+#define CDC_SCAN_DYN 0
+#endif
+#ifdef CDC_SCAN_MAXW  // min waves per SIMD -> VGPR cap 512 / CDC_SCAN_MAXW (needs CDC_SCAN_DYN)
+#define CDC_SCAN_VGPR_ATTR __attribute__((amdgpu_flat_work_group_size(1, kW * 64), amdgpu_waves_per_eu(CDC_SCAN_MAXW)))
+#else
+#define CDC_SCAN_VGPR_ATTR __launch_bounds__(kW * 64, 1)
+#endif
 template <bool kAlign, int kW, int kLook, int kMode>
-__global__ __launch_bounds__(kW * 64, 1) void scan_kernel(const StreamTable st, const FastParams fp,
+__global__ CDC_SCAN_VGPR_ATTR void scan_kernel(const StreamTable st, const FastParams fp,
                                                            const uint64_t *__restrict__ gear,
                                                            const Candidates cand, const Compact cp) {
+#if CDC_SCAN_DYN
+    extern __shared__ uint4 scan_dyn[];  // (dynamic: the compiler then honours the VGPR cap)
+    ScanLds<kW> &L = *reinterpret_cast<ScanLds<kW> *>(scan_dyn);
+#else
     __shared__ ScanLds<kW> L;
+#endif
     const uint64_t *tab = L.tab;
     for (int i = threadIdx.x; i < 256 * kCopies; i += kW * 64)
         L.tab[i] = gear[i / kCopies] << fp.tshift;  // pre-shifted GEAR (see FastParams)
@@ -1736,7 +1749,10 @@ __device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) {
 // timing experiments only, 0 in every real run: 1 = walks start at the span
 // start (no warm-up: nearly every boundary re-walks), 2 = every wave takes the
 // dense (global record list) path, 128 = phase timings into the stats.
-__global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTable st, const FastParams fp,
+#ifndef CDC_RES_ATTR
+#define CDC_RES_ATTR __launch_bounds__(kResThreads, 2)
+#endif
+__global__ CDC_RES_ATTR void resolve_kernel(const StreamTable st, const FastParams fp,
                                                               const uint64_t *__restrict__ gear,
                                                               const Candidates cand, const Chains ch,
                                                               const Compact cp, const Resolve rs,
@@ -2064,6 +2080,30 @@ __global__ __launch_bounds__(kResThreads, 2) void resolve_kernel(const StreamTab
 
 }  // namespace
 
+#ifdef CDC_OVL
+namespace ovl {  // the overlap set (fastcdc_ovl.hip): this file built again with its sizes
+#endif
+
+// Dynamic LDS of the scan (CDC_SCAN_DYN): the size and, once per kernel, the
+// attribute that admits more than 64 KiB.
+template <bool kAlign, int kW, int kLook, int kMode>
+static hipError_t scan_launch(unsigned grid, const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
+                              const Candidates &cand, const Compact &cp, hipStream_t s) {
+    size_t lds = 0;
+    if (CDC_SCAN_DYN) {
+        lds = sizeof(ScanLds<kW>);
+        static bool attr = false;
+        if (!attr) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&scan_kernel<kAlign, kW, kLook, kMode>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+    }
+    scan_kernel<kAlign, kW, kLook, kMode><<<grid, kW * 64, lds, s>>>(st, fp, d_gear, cand, cp);
+    return hipSuccess;
+}
+
 hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
                        const Candidates &cand, const Compact &cp, const uint64_t *d_tails, uint32_t n_tails,
                        int num_cus, hipStream_t s) {
@@ -2090,15 +2130,16 @@ hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64
     }
     const uint64_t groups = (st.total_spans + W - 1) / W;
     const unsigned grid = (unsigned)(groups < (uint64_t)num_cus ? groups : (uint64_t)num_cus);
+    hipError_t e;
     if (mode == 1 && fp.cm_align)
-        scan_kernel<true, W, K, 1><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+        e = scan_launch<true, W, K, 1>(grid, st, fp, d_gear, cand, cp, s);
     else if (mode == 2 && fp.cm_align)
-        scan_kernel<true, W, K, 2><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+        e = scan_launch<true, W, K, 2>(grid, st, fp, d_gear, cand, cp, s);
     else if (fp.cm_align)
-        scan_kernel<true, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
+        e = scan_launch<true, W, K, 0>(grid, st, fp, d_gear, cand, cp, s);
     else
-        scan_kernel<false, W, K, 0><<<grid, W * 64, 0, s>>>(st, fp, d_gear, cand, cp);
-    return hipGetLastError();
+        e = scan_launch<false, W, K, 0>(grid, st, fp, d_gear, cand, cp, s);
+    return e != hipSuccess ? e : hipGetLastError();
 }
 
 uint64_t resolve_blocks(uint64_t spans) { return (spans + kBlockSpans - 1) / kBlockSpans; }
@@ -2112,5 +2153,8 @@ hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uin
     return hipGetLastError();
 }
 
+#ifdef CDC_OVL
+}  // namespace ovl
+#endif
 }  // namespace p3
 }  // namespace cdc

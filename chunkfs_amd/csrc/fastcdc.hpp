@@ -60,5 +60,20 @@ hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uin
                           const Candidates &cand, const Chains &ch, const Compact &cp, const Resolve &rs,
                           void *d_out, uint64_t out_cap, hipStream_t s);
 
+// The overlap set (fastcdc_ovl.hip: the same kernels at other sizes) for
+// back-to-back batches whose resolve runs on a second stream beside the next
+// batch's scan: the scan at 8 waves per CU, <= 128 VGPRs and 112 KiB of LDS
+// leaves each CU room for one 4-wave resolve block (<= 256 VGPRs per lane,
+// 46 KiB of LDS, 32 spans per block).
+namespace ovl {
+uint64_t resolve_blocks(uint64_t spans);
+hipError_t launch_scan(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
+                       const Candidates &cand, const Compact &cp, const uint64_t *d_tails, uint32_t n_tails,
+                       int num_cus, hipStream_t s);
+hipError_t launch_resolve(const StreamTable &st, const FastParams &fp, const uint64_t *d_gear,
+                          const Candidates &cand, const Chains &ch, const Compact &cp, const Resolve &rs,
+                          void *d_out, uint64_t out_cap, hipStream_t s);
+}  // namespace ovl
+
 }  // namespace p3
 }  // namespace cdc

@@ -363,6 +363,10 @@ int64_t Engine::chunk_host(const uint8_t *data, size_t len, cdc_chunk_t *out, si
     }
     if (len == 0) return 0;  // FastCDC iterator yields nothing; FSChunker loop never runs
     HIP_TRY(hipSetDevice(device_));
+    if (fb_any_) {  // async batches first: the small path reuses host staging block 0
+        const int64_t r = drain_implicit();
+        if (r < 0) return r;
+    }
     const double t0 = now_s();
     int rc = ensure_ring();
     if (!rc) rc = ensure_device_data(len);

@@ -6,14 +6,16 @@
 // after chunking.
 //
 // Layout: one LANE per chunk (a chunk's 64-byte blocks are inherently
-// sequential).  Chunk lengths vary (min..max), so lanes are refilled
+// sequential); a launch takes the chunks of many streams at once (a batch:
+// cdc_sha256_batch_device), so a 4 GiB archive is one launch of ~1M lanes.  Chunk lengths vary (min..max), so lanes are refilled
 // dynamically: after every block, lanes whose chunk is done take the next
 // chunk indices from a global counter (one atomic per wave per refill), and a
 // wave leaves only when the counter is exhausted and all its lanes are idle.
 // Each block's 16 big-endian words are built from 17 aligned dwords with one
 // v_perm_b32 per word (funnel shift + byte swap in one instruction); the last
-// one or two blocks (0x80 terminator, bit length) take a guarded byte path.
-// Integer work only: Ch/Maj lower to v_bitop3_b32, rotations to v_alignbit.
+// one or two blocks (0x80 terminator, bit length) are masked in registers.
+// Integer work only: Ch/Maj and the sigmas' three-way XORs lower to
+// v_bitop3_b32, rotations to v_alignbit.
 #include "sha256.hpp"
 
 namespace cdc {
@@ -35,9 +37,17 @@ constexpr uint32_t kH0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
 constexpr int kShaThreads = 256;
 
 typedef const __attribute__((address_space(1))) uint32_t g_u32;
-typedef const __attribute__((address_space(1))) uint8_t g_u8;
+typedef const __attribute__((address_space(1))) uint64_t g_u64c;
+// 16-byte loads at a 4-byte-aligned address (a chunk starts at any byte).
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef const __attribute__((address_space(1))) u32x4_a4 g_u32x4_a4;
 
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_rotateright32(x, n); }
+// Three-input XOR in one v_bitop3_b32 (truth table 0x96); LLVM emits two
+// v_xor_b32 for the plain expression.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 __device__ __forceinline__ void compress(uint32_t H[8], uint32_t W[16]) {
     uint32_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
@@ -48,15 +58,15 @@ __device__ __forceinline__ void compress(uint32_t H[8], uint32_t W[16]) {
             w = W[t];
         } else {
             const uint32_t w15 = W[(t + 1) & 15], w2 = W[(t + 14) & 15];
-            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
             w = W[t & 15] + s0 + W[(t + 9) & 15] + s1;
             W[t & 15] = w;
         }
-        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
         const uint32_t ch = (e & f) ^ (~e & g);
         const uint32_t t1 = h + S1 + ch + kK[t] + w;
-        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
         const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
         const uint32_t t2 = S0 + mj;
         h = g;
@@ -74,86 +84,139 @@ __device__ __forceinline__ void compress(uint32_t H[8], uint32_t W[16]) {
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
-__global__ __launch_bounds__(kShaThreads) void sha256_kernel(const uint8_t *__restrict__ data,
-                                                             const cdc_chunk_pod *__restrict__ chunks,
-                                                             uint64_t n_chunks, uint32_t *__restrict__ digests,
-                                                             unsigned long long *counter) {
+// Work distribution: a lane hashes one chunk at a time and keeps the NEXT
+// chunk claimed and described ahead of time, in a three-stage pipeline that
+// advances one stage per block step -- (1) claim an index (one atomic per wave
+// for all lanes that need one), (2) find its stream (binary search of the
+// batch's first[] in LDS) and issue the loads of its record and its
+// successor's, (3) take it over when the current chunk ends.  Each stage's
+// latency (L2 atomic, record loads) then hides behind a step of compression
+// instead of stalling the wave at every refill (~2 of 3 steps see a lane
+// finish: 64 lanes, ~65 blocks per 4 KiB chunk).  Waves leave when every lane
+// is idle and the counter is exhausted.
+//
+// A block of the message is 17 dwords from the 4-byte-aligned address below
+// it, realigned by one v_perm per big-endian word; the 68-byte window is read
+// with four 16-byte loads and one dword load whenever it cannot run past
+// readable memory: inside the chunk, or past its end into the next chunk of
+// the same stream when that one is contiguous and >= 68 bytes ("over": every
+// chunk but the last one or two of a stream).  Otherwise (a stream's last
+// chunk tail) each dword is loaded only if it holds a chunk byte.  The words
+// of the last one or two blocks (0x80 terminator, zeros, 64-bit bit length)
+// are masked in registers, without byte loops.
+constexpr uint32_t kShaLdsStreams = 2048;  // stream tables up to this many streams are staged in LDS
+
+template <bool kLds>
+__global__ __launch_bounds__(kShaThreads) void sha256_kernel(const ShaBatch j) {
+    extern __shared__ uint64_t tab[];  // (kLds) first[n+1] ++ base[n], (2n+1) * 8 bytes of dynamic LDS
+    const uint64_t *first = j.first, *sbase = j.base;
+    if constexpr (kLds) {
+        for (uint32_t i = threadIdx.x; i <= 2 * j.n_streams; i += kShaThreads)
+            tab[i] = i <= j.n_streams ? *(g_u64c *)(j.first + i) : *(g_u64c *)(j.base + (i - j.n_streams - 1));
+        __syncthreads();
+        first = tab;
+        sbase = tab + j.n_streams + 1;
+    }
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t lanemask_lt = (1ull << lane) - 1;
-    uint64_t ci = ~0ull;      // this lane's chunk (~0: idle)
-    uint64_t start = 0, len = 0, blk = 0, nblk = 0;
+    // current chunk
+    uint64_t ci = ~0ull, src = 0, len = 0, blk = 0, nblk = 0;
+    bool over = false;
     uint32_t H[8];
+    // next chunk: stage 0 = none, 1 = index claimed, 2 = described, 3 = counter exhausted
+    uint32_t nst = 0;
+    uint64_t ni = 0, nsrc = 0;
+    cdc_chunk_pod nc{}, nn{};
+    bool nhas = false;
     for (;;) {
-        // Refill idle lanes: one atomic per wave, indices handed out by rank.
-        const uint64_t idle = __ballot(ci == ~0ull);
-        if (idle) {
-            const uint32_t k = (uint32_t)__popcll(idle);
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(counter, (unsigned long long)k);
-            base = __shfl(base, 0);
-            if (ci == ~0ull) {
-                const uint64_t mine = base + (uint64_t)__popcll(idle & lanemask_lt);
-                if (mine < n_chunks) {
-                    ci = mine;
-                    const cdc_chunk_pod c = chunks[mine];
-                    start = c.offset;
-                    len = c.length;
-                    blk = 0;
-                    nblk = (len + 9 + 63) / 64;  // message + 0x80 + 64-bit length, padded
+        // (3) take the next chunk over when the current one is done
+        if (ci == ~0ull && nst == 2) {
+            ci = ni;
+            src = nsrc + nc.offset;
+            len = nc.length;
+            over = nhas && nn.offset == nc.offset + nc.length && nn.length >= 68;
+            blk = 0;
+            nblk = (len + 9 + 63) / 64;  // message + 0x80 + 64-bit length, padded
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) H[i] = kH0[i];
-                }
+            for (int i = 0; i < 8; ++i) H[i] = kH0[i];
+            nst = 0;
+        }
+        // (2) describe a claimed index: its stream, and the loads of its record
+        if (nst == 1) {
+            uint32_t lo = 0, hi = j.n_streams;  // largest s with first[s] <= ni
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (first[mid] <= ni) lo = mid; else hi = mid;
+            }
+            nsrc = sbase[lo];
+            nhas = ni + 1 < first[lo + 1];
+            nc = j.chunks[ni];
+            nn = j.chunks[nhas ? ni + 1 : ni];
+            nst = 2;
+        }
+        // (1) claim indices for the lanes with an empty next stage
+        const uint64_t want = __ballot(nst == 0);
+        if (want) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(j.counter, (unsigned long long)__popcll(want));
+            base = __shfl(base, 0);
+            if (nst == 0) {
+                ni = base + (uint64_t)__popcll(want & lanemask_lt);
+                nst = ni < j.n_chunks ? 1u : 3u;
             }
         }
-        if (__ballot(ci != ~0ull) == 0) break;  // counter exhausted and every lane idle
+        if (__ballot(ci != ~0ull || nst == 1 || nst == 2) == 0) break;  // nothing left anywhere in the wave
         if (ci != ~0ull) {
-            uint32_t W[16];
             const uint64_t p = 64 * blk;  // block start within the chunk
-            if (p + 64 <= len) {
-                // Full data block: 17 aligned dwords, one v_perm per big-endian word.
-                const uint64_t a = start + p;
-                const uint64_t al = a & ~3ull;
-                const uint32_t sh = (uint32_t)(a - al);
-                g_u32 *src = (g_u32 *)(data + al);
-                uint32_t d[17];
+            const uint64_t a = src + p;
+            const uint32_t sh = (uint32_t)(a & 3);
+            const uint64_t al = a - sh;
+            uint32_t d[17];
+            if (p >= len) {  // a padding-only block
 #pragma unroll
-                for (int i = 0; i < 16; ++i) d[i] = src[i];
-                d[16] = 0;
-                if (sh) {  // the block's last bytes; never read past the chunk
-                    if (al + 68 <= start + len) {
-                        d[16] = src[16];
-                    } else {
-                        g_u8 *b = (g_u8 *)(data + al + 64);
-                        for (uint32_t j = 0; j < sh; ++j) d[16] |= (uint32_t)b[j] << (8 * j);
-                    }
+                for (int i = 0; i < 17; ++i) d[i] = 0;
+            } else if (over || p + 68 <= len) {
+                g_u32x4_a4 *q = (g_u32x4_a4 *)al;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const u32x4_a4 v = q[i];
+                    d[4 * i] = v.x;
+                    d[4 * i + 1] = v.y;
+                    d[4 * i + 2] = v.z;
+                    d[4 * i + 3] = v.w;
                 }
-                const uint32_t sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+                d[16] = sh ? *(g_u32 *)(al + 64) : 0u;
             } else {
-                // Tail: remaining bytes, 0x80, zeros, bit length in the last 8 bytes.
-                g_u8 *src = (g_u8 *)(data + start);
-                const uint64_t bits = len * 8;
+                const uint64_t end = src + len;
+#pragma unroll
+                for (int i = 0; i < 17; ++i) d[i] = al + 4 * i < end ? *(g_u32 *)(al + 4 * i) : 0u;
+            }
+            const uint32_t sel = (sh << 24) | ((sh + 1) << 16) | ((sh + 2) << 8) | (sh + 3);
+            uint32_t W[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) W[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+            if (__ballot(p + 64 > len)) {
+                // Word i holds message bytes p+4i .. p+4i+3: r = len - (p+4i)
+                // of them are data; the first one past the data is 0x80.
+                const int64_t r0 = (int64_t)len - (int64_t)p;
                 const bool last = blk + 1 == nblk;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    uint32_t w = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint64_t q = p + 4 * i + j;
-                        uint32_t byte = 0;
-                        if (q < len) byte = src[q];
-                        else if (q == len) byte = 0x80u;
-                        w = (w << 8) | byte;
-                    }
-                    if (last && i == 14) w = (uint32_t)(bits >> 32);
-                    if (last && i == 15) w = (uint32_t)bits;
-                    W[i] = w;
+                    const int64_t r = r0 - 4 * i;
+                    const uint32_t rk = (uint32_t)(r < 0 ? 0 : r > 4 ? 4 : r);  // data bytes kept
+                    const uint32_t rp = (uint32_t)(r < 0 ? 5 : r > 5 ? 5 : r);  // 0x80 position (>= 4: none)
+                    const uint32_t keep = (uint32_t)~(0xFFFFFFFFull >> (8 * rk));
+                    const uint32_t pad = (uint32_t)(0x80000000ull >> (8 * rp));
+                    W[i] = (W[i] & keep) | pad;
+                }
+                if (last) {
+                    W[14] = (uint32_t)(len >> 29);  // bit length, big-endian 64-bit
+                    W[15] = (uint32_t)(len << 3);
                 }
             }
             compress(H, W);
             if (++blk == nblk) {
-                uint32_t *o = digests + 8 * ci;
+                uint32_t *o = j.digests + 8 * ci;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) o[i] = bswap(H[i]);  // big-endian digest bytes
                 ci = ~0ull;
@@ -164,18 +227,18 @@ __global__ __launch_bounds__(kShaThreads) void sha256_kernel(const uint8_t *__re
 
 }  // namespace
 
-hipError_t launch_sha256(const uint8_t *d_data, const void *d_chunks, uint64_t n_chunks,
-                         uint8_t *d_digests, unsigned long long *d_counter, int num_cus,
-                         hipStream_t s) {
-    if (!n_chunks) return hipSuccess;
-    hipError_t e = hipMemsetAsync(d_counter, 0, sizeof(unsigned long long), s);
+hipError_t launch_sha256(const ShaBatch &b, int num_cus, hipStream_t s) {
+    if (!b.n_chunks) return hipSuccess;
+    hipError_t e = hipMemsetAsync(b.counter, 0, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    const uint64_t waves = (n_chunks + 63) / 64;
+    const uint64_t waves = (b.n_chunks + 63) / 64;
     const uint64_t want = (waves + 3) / 4;
     const uint64_t cap = (uint64_t)num_cus * 8;  // resident blocks: lanes refill in place
     const unsigned grid = (unsigned)(want < cap ? want : cap);
-    sha256_kernel<<<grid, kShaThreads, 0, s>>>(d_data, reinterpret_cast<const cdc_chunk_pod *>(d_chunks),
-                                               n_chunks, reinterpret_cast<uint32_t *>(d_digests), d_counter);
+    if (b.n_streams <= kShaLdsStreams)
+        sha256_kernel<true><<<grid, kShaThreads, (2 * b.n_streams + 1) * sizeof(uint64_t), s>>>(b);
+    else
+        sha256_kernel<false><<<grid, kShaThreads, 0, s>>>(b);
     return hipGetLastError();
 }
 

@@ -7,10 +7,20 @@
 
 namespace cdc {
 
-// digests[32*i .. 32*i+32) = SHA-256(d_data[chunks[i].offset .. +length)).
-// d_counter: one device u64 of scratch (work distribution).
-hipError_t launch_sha256(const uint8_t *d_data, const void *d_chunks, uint64_t n_chunks,
-                         uint8_t *d_digests, unsigned long long *d_counter, int num_cus,
-                         hipStream_t s);
+// A batch: the chunks of n_streams streams, stream i's chunks at
+// chunks[first[i] .. first[i+1]) with offsets relative to base[i] (DEVICE
+// arrays).  digests[8*k .. 8*k+8) (u32, big-endian bytes) = SHA-256 of chunk
+// k.  counter: one device u64 of scratch (work distribution).
+struct ShaBatch {
+    const cdc_chunk_pod *chunks;
+    uint64_t n_chunks;
+    const uint64_t *first;  // [n_streams + 1]
+    const uint64_t *base;   // [n_streams]: stream base addresses (4-byte aligned)
+    uint32_t n_streams;
+    uint32_t *digests;
+    unsigned long long *counter;
+};
+
+hipError_t launch_sha256(const ShaBatch &b, int num_cus, hipStream_t s);
 
 }  // namespace cdc

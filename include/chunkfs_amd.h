@@ -28,8 +28,9 @@ extern "C" {
 /* 2: cdc_last_timing takes the caller's sizeof(cdc_timing_t) (the struct
  *    may grow; fields are only ever appended); cdc_abi_version().
  * 3: cdc_timing_t.path / .timed appended; cdc_chunk_batch_device_async,
- *    cdc_batch_sync. */
-#define CHUNKFS_AMD_ABI_VERSION 3
+ *    cdc_batch_sync.
+ * 4: cdc_sha256_batch_device. */
+#define CHUNKFS_AMD_ABI_VERSION 4
 
 /* Chunk{offset,length} -- reference src/lib.rs:43-47 (usize fields; u64 here). */
 typedef struct cdc_chunk {
@@ -184,7 +185,7 @@ typedef struct cdc_timing {
     uint32_t overflow_spans; /* spans whose candidate list overflowed */
     uint64_t candidates;     /* candidate positions emitted by the scan */
     uint64_t bytes;          /* input bytes of the batch */
-    double hash_ms;          /* last cdc_sha256_chunks_device / cdc_chunk_and_hash kernel time */
+    double hash_ms;          /* last cdc_sha256_chunks_device / _batch_device / cdc_chunk_and_hash kernel time */
     uint64_t walk_fallback_steps; /* chain-walk steps without a precomputed record link */
     uint32_t path;           /* CDC_PATH_*: which engine path ran the batch */
     uint32_t timed;          /* 1: the *_ms fields were measured (HIP events); 0: not timed */
@@ -254,6 +255,18 @@ int64_t cdc_write_finish(cdc_handle_t *h, uint64_t *span_lengths, size_t cap,
 int cdc_sha256_chunks_device(cdc_handle_t *h, const uint8_t *d_data,
                              const cdc_chunk_t *d_chunks, size_t n_chunks,
                              uint8_t *d_digests, void *hip_stream);
+
+/* The same over a batch of streams in one launch -- e.g. the output of
+ * cdc_chunk_batch_device: stream i's chunks are d_chunks[first[i] ..
+ * first[i+1]) with offsets relative to d_streams[i]; first[0] must be 0.
+ * d_streams (n_streams device pointers, 4-byte aligned) and first
+ * (n_streams + 1 entries) are HOST arrays; d_chunks / d_digests are DEVICE
+ * arrays of first[n_streams] entries (32-byte digests, chunk order).  Each
+ * stream's chunks must lie inside its buffer.  Synchronises hip_stream. */
+int cdc_sha256_batch_device(cdc_handle_t *h, size_t n_streams,
+                            const uint8_t *const *d_streams, const uint64_t *first,
+                            const cdc_chunk_t *d_chunks, uint8_t *d_digests,
+                            void *hip_stream);
 
 /* chunk_data + SHA-256 of each chunk on a HOST buffer: as cdc_chunk_data, and
  * digests[32*i ..] for the first min(count, cap) chunks. */

@@ -85,3 +85,64 @@ def test_config1_fixed_8k_64mib_sha256():
         unique.setdefault(bytes(d), int(ln))  # database.rs:74-77: first insert wins
     assert n / sum(unique.values()) == 1.0
     assert sum(unique.values()) / len(unique) == 8192.0
+
+
+def _batch_check(ch, bufs, lens, first, out, torch):
+    n = int(first[-1])
+    dig = torch.empty((max(n, 1), 32), dtype=torch.uint8, device="cuda")
+    ch.sha256_batch_device([b.data_ptr() for b in bufs], first, out.data_ptr(), dig.data_ptr())
+    got = dig[:n].cpu().numpy()
+    allc = out[:n].cpu().numpy().view(np.uint64)
+    for i, (b, ln) in enumerate(zip(bufs, lens)):
+        a, z = int(first[i]), int(first[i + 1])
+        assert (got[a:z] == _digests(b[:ln].cpu().numpy(), allc[a:z])).all(), f"stream {i}"
+
+
+def test_sha256_batch_multi_stream_rabin():
+    """cdc_sha256_batch_device over a multi-stream Rabin batch (config 3's
+    shape): one launch, per-stream bases, empty and tiny streams included."""
+    import torch
+    import chunkfs_amd as c
+    sizes = (2048, 4096, 8192)
+    lens = [(6 << 20) + 5, 0, 1, 67, 4097, (3 << 20) + 1, 130]
+    bufs = [torch.from_numpy(oracle.splitmix64_bytes(max(n, 1), 40 + i)).cuda() for i, n in enumerate(lens)]
+    ch = c.RabinChunker(c.SizeParams(*sizes))
+    cap = ch.batch_max_chunks(lens)
+    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda")
+    first = ch.chunk_batch_device([b.data_ptr() for b in bufs], lens, out.data_ptr(), cap)
+    _batch_check(ch, bufs, lens, first, out, torch)
+    assert ch.last_timing()["hash_ms"] > 0
+
+
+def test_sha256_batch_contiguous_short_neighbours():
+    """Contiguous chunks whose successors are shorter / longer than the
+    68-byte over-read window, ending exactly at the end of the data, at odd
+    offsets: every load-path choice of the kernel."""
+    import torch
+    import chunkfs_amd as c
+    pat = [70, 67, 68, 69, 1, 0, 200, 3, 64, 55, 56, 119, 120, 4096, 66, 5000, 2, 1000]
+    bufs, lens_b, chunk_lists = [], [], []
+    for k, skew in enumerate((0, 1, 2, 3)):
+        lens_c = pat[k:] + pat[:k]
+        total = skew + sum(lens_c)
+        bufs.append(torch.from_numpy(oracle.splitmix64_bytes(total, 90 + k)).cuda())
+        lens_b.append(total)
+        offs = np.cumsum([skew] + lens_c[:-1])
+        chunk_lists.append(np.stack([offs, lens_c], axis=1).astype(np.uint64))
+    first = np.cumsum([0] + [len(cl) for cl in chunk_lists]).astype(np.uint64)
+    out = torch.from_numpy(np.concatenate(chunk_lists).view(np.int64)).cuda()
+    ch = c.FastChunker(c.SizeParams(4096, 8192, 16384))
+    _batch_check(ch, bufs, lens_b, first, out, torch)
+
+
+def test_sha256_batch_rejects_bad_tables():
+    import torch
+    import chunkfs_amd as c
+    ch = c.FastChunker(c.SizeParams(4096, 8192, 16384))
+    b = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    out = torch.zeros((2, 2), dtype=torch.int64, device="cuda")
+    dig = torch.empty((2, 32), dtype=torch.uint8, device="cuda")
+    with pytest.raises(c.CdcError):
+        ch.sha256_batch_device([b.data_ptr()], [1, 2], out.data_ptr(), dig.data_ptr())  # first[0] != 0
+    with pytest.raises(c.CdcError):
+        ch.sha256_batch_device([b.data_ptr(), b.data_ptr()], [0, 2, 1], out.data_ptr(), dig.data_ptr())
