@@ -188,7 +188,7 @@ int Engine::init() {
     for (auto &slot : tev_)
         for (auto &ev : slot) HIP_TRY(hipEventCreate(&ev));
     HIP_TRY(hipMalloc(&d_gear_, 256 * sizeof(uint64_t)));
-    HIP_TRY(hipMalloc(&d_counter_, sizeof(unsigned long long)));
+    HIP_TRY(hipMalloc(&d_counter_, (1 + kShaBuckets) * sizeof(unsigned long long)));  // SHA-256 counter + histogram
     HIP_TRY(hipMemcpy(d_gear_, CHUNKFS_AMD_GEAR, 256 * sizeof(uint64_t), hipMemcpyHostToDevice));
     return CDC_OK;
 }
@@ -206,6 +206,7 @@ Engine::~Engine() {
     (void)hipFree(d_dig_);
     (void)hipFree(d_sha_tab_);
     (void)hipHostFree(h_sha_tab_);
+    (void)hipFree(d_sha_order_);
     (void)hipFree(d_counter_);
     (void)hipFree(d_wtabs_);
     (void)hipFree(wws_);
@@ -961,6 +962,10 @@ int Engine::sha256_batch(size_t n, const uint8_t *const *d_streams, const uint64
         }
     }
     const uint64_t total = first[n];
+    if (total >= (1ull << 32)) {
+        set_error("cdc_sha256_batch_device: more than 2^32 - 1 chunks in one batch");
+        return CDC_EINVAL;
+    }
     if (total && (!d_chunks || !d_digests)) {
         set_error("cdc_sha256_chunks_device: NULL argument");
         return CDC_EINVAL;
@@ -998,6 +1003,15 @@ int Engine::sha256_batch(size_t n, const uint8_t *const *d_streams, const uint64
     b.n_streams = (uint32_t)n;
     b.digests = reinterpret_cast<uint32_t *>(d_digests);
     b.counter = d_counter_;
+    if (sha_order_cap_ < total) {
+        (void)hipFree(d_sha_order_);
+        d_sha_order_ = nullptr;
+        sha_order_cap_ = 0;
+        const uint64_t want = total + total / 8 + 1024;
+        HIP_TRY(hipMalloc(&d_sha_order_, want * sizeof(uint32_t)));
+        sha_order_cap_ = want;
+    }
+    b.order = d_sha_order_;
     HIP_TRY(hipEventRecord(ev_[3], st));
     HIP_TRY(launch_sha256(b, num_cus_, st));
     HIP_TRY(hipEventRecord(ev_[2], st));

@@ -332,6 +332,8 @@ class Engine {
     unsigned long long *d_counter_ = nullptr;  // SHA-256 work counter
     uint64_t *d_sha_tab_ = nullptr, *h_sha_tab_ = nullptr;  // SHA-256 batch stream table: first[n+1] ++ bases[n]
     size_t sha_tab_cap_ = 0;
+    uint32_t *d_sha_order_ = nullptr;  // SHA-256 claim order (longest chunk first)
+    uint64_t sha_order_cap_ = 0;
 
     cdc_timing_t timing_{};
     bool timing_pending_ = false;  // FastCDC events not read yet (see timing())
