@@ -1239,6 +1239,7 @@ int Engine::init_walk(const uint32_t *seq) {
     wp.ahead = 1;
     wp.bits_fine = 1;
     if (const char *f = std::getenv("CHUNKFS_AMD_BITS_FINE")) wp.bits_fine = std::atoi(f) != 0 ? 1u : 0u;
+    if (const char *f = std::getenv("CHUNKFS_AMD_WALK_FUSED")) walk_fused_ = std::atoi(f) != 0;
     wp.cap = (uint32_t)((1ull << seg_log2_) / min_ + 2);
     // Link mode (Rabin, UltraCDC, LeapCDC): candidate lists of ~4x
     // the expected count per segment -- Rabin hits 2^-round(log2 avg) per
@@ -1325,7 +1326,7 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     };
     const size_t oE = take(S * 8), oX = take(S * 8), oXs = take(S * 8), oEs = take(S * 8), oP = take((S + 1) * 8);
     const size_t oN = take(S * 4), oL = take(S * (size_t)wp_.cap * 8), oB = take((nb + 1) * 8);
-    const size_t oF = take((N + 1) * 8), oG = take((4 + 4 * walk::kMaxFixRounds) * 8);
+    const size_t oF = take((N + 1) * 8), oG = take((4 + 4 * walk::kMaxFixRounds) * 8), oGo = take(16);
     const size_t oBM = take(S * (size_t)wp_.seg_words * wp_.nbm * 8);  // predicate bitmaps
     const bool jt = algo_ == CDC_ALGO_LEAP && wp_.wave;
     const size_t oJT = take(jt ? S * (size_t)wp_.seg_words * 24 : 0);  // LeapCDC word tables
@@ -1359,6 +1360,8 @@ int Engine::ensure_walk_workspace(uint64_t segs, size_t n) {
     wst_.bsum = reinterpret_cast<uint64_t *>(b + oB);
     wst_.first = reinterpret_cast<uint64_t *>(b + oF);
     wst_.flags = reinterpret_cast<unsigned long long *>(b + oG);
+    walk_go_ = reinterpret_cast<uint64_t *>(b + oGo);
+    walk_flags_clean_ = false;  // (fresh memory: the next call initialises the flag blocks)
     wp_.bm = wp_.nbm ? reinterpret_cast<uint64_t *>(b + oBM) : nullptr;
     wp_.jt = jt ? reinterpret_cast<uint8_t *>(b + oJT) : nullptr;
     wp_.jt8 = jt ? reinterpret_cast<uint16_t *>(b + oJ8) : nullptr;
@@ -1387,7 +1390,10 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     uint64_t *h_rf = h_flags + 4;
     const uint32_t R = max_rounds_ < walk::kMaxFixRounds ? max_rounds_ : walk::kMaxFixRounds;
     HIP_TRY(hipEventRecord(ev_[0], s));
-    HIP_TRY(walk::launch_flags_init(wst_.flags, R, s));
+    // (the previous call's end kernel resets the flag blocks when it ends
+    // the call: then no init launch here)
+    if (!walk_flags_clean_) HIP_TRY(walk::launch_flags_init(wst_.flags, R, s));
+    walk_flags_clean_ = false;
     static const bool diag = std::getenv("CHUNKFS_AMD_WALKDIAG") != nullptr;  // phase times + candidates
     auto lap = [&](const char *what) -> int {
         if (!diag) return CDC_OK;
@@ -1434,7 +1440,7 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     constexpr uint32_t kGroup = 4;
     unsigned long long *rf = wst_.flags + 4;
     uint64_t rewalked = 0, round_errors = 0;
-    bool settled = false, quiet_stop = false, queued = false;
+    bool settled = false, quiet_stop = false, queued = false, fused = false;
     uint32_t launched = 0, last_round = 0;
     while (launched < R && !settled) {
         const uint32_t grp = launched == 0 ? walk::kFirstGroupRounds : kGroup;
@@ -1448,7 +1454,7 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
             ws.flags = rf + 4 * r;
             ws.gate = r ? rf + 4 * (r - 1) : nullptr;
             const auto t0 = std::chrono::steady_clock::now();
-            HIP_TRY(walk::launch_fix(st, wp_, ws, s));
+            HIP_TRY(walk::launch_fix(st, wp_, ws, s, r != 0));  // (round 0's snapshot: written by the walk)
             if (diag) {
                 HIP_TRY(hipStreamSynchronize(s));
                 std::fprintf(stderr, "  walkdiag round %u %.3f ms\n", r,
@@ -1457,11 +1463,21 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
         }
         queued = launched == 0 && !diag;
         launched = end;
-        if (queued) {
-            HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s, rf, launched));
-            HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+        // Fused end (walk::launch_finish_emit): the prefix, first[] and the
+        // flag blocks go straight into the host staging block -- no D2H
+        // copies -- and the flags are reset for the next call when it ends
+        // this one.
+        fused = queued && walk_fused_ && walk::finish_fits(st);
+        if (fused) {
+            HIP_TRY(walk::launch_finish_emit(st, wp_, wst_, d_out, out_cap_, s, rf, launched, launched, walk_go_,
+                                             h_first, h_flags));
+        } else {
+            if (queued) {
+                HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s, rf, launched));
+                HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+            }
+            HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, (4 + (size_t)launched * 4) * 8, hipMemcpyDeviceToHost, s));
         }
-        HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, (4 + (size_t)launched * 4) * 8, hipMemcpyDeviceToHost, s));
         if (queued) HIP_TRY(hipEventRecord(ev_[2], s));
         HIP_TRY(hipStreamSynchronize(s));
         // The first round that settled everything, or whose changed exits
@@ -1505,7 +1521,9 @@ int Engine::run_walk(const StreamTable &st, cdc_chunk_t *d_out, size_t n, uint64
     // The gated output queued after the first group ran on the device exactly
     // when that group settled by the same rule (emit_skips), i.e. when the
     // loop stopped after it: launched == kFirstGroupRounds.
-    if (!(queued && settled && launched == walk::kFirstGroupRounds)) {  // (else the gated output already ran)
+    const bool gated_ran = queued && settled && launched == walk::kFirstGroupRounds;
+    walk_flags_clean_ = gated_ran && fused;  // (finish_kernel reset them)
+    if (!gated_ran) {  // (else the gated output already ran)
         HIP_TRY(walk::launch_emit(st, wp_, wst_, d_out, out_cap_, s));
         HIP_TRY(hipMemcpyAsync(h_flags, wst_.flags, 4 * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(h_first, wst_.first, (n + 1) * 8, hipMemcpyDeviceToHost, s));

@@ -370,6 +370,9 @@ class Engine {
     uint64_t wws_segs_ = 0;
     size_t wws_streams_ = 0;
     walk::WalkState wst_{};
+    uint64_t *walk_go_ = nullptr;     // finish_kernel's verdict word for the gated emit
+    bool walk_flags_clean_ = false;   // the flag blocks hold the init pattern (the last call's end kernel reset them)
+    bool walk_fused_ = true;          // fused end kernel (CHUNKFS_AMD_WALK_FUSED=0: sum / prefix / first + copies, A/B)
 };
 
 void set_error(const std::string &msg);

@@ -534,6 +534,7 @@ template <int kAlgo, bool kBits>
 __device__ void walk_from(uint64_t c, uint64_t g, uint64_t seg_end, uint64_t len, Reader &r,
                           const WalkParams &wp, const Tabs &T, const WalkState &ws, Hop &hp) {
     ws.E[g] = c;
+    ws.Es[g] = c;  // (round 0's snapshot: launch_fix skips its snap_kernel)
     uint32_t cnt = 0;
     uint64_t *list = ws.list + g * wp.cap;
     while (c < seg_end) {
@@ -542,6 +543,7 @@ __device__ void walk_from(uint64_t c, uint64_t g, uint64_t seg_end, uint64_t len
         c = advance<kAlgo, kBits>(r, c, len, hp, wp, T);
     }
     ws.X[g] = c;
+    ws.Xs[g] = c;
     ws.N[g] = cnt;
     if (cnt > wp.cap) atomicAdd(&ws.flags[1], 1ull);
 }
@@ -1405,7 +1407,10 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
             take_run<kAlgo>(B, rs, d, pk, c, len, off, wp, lane, nullptr, skip);
         }
     }
-    if (lane == 0) ws.E[g] = c;
+    if (lane == 0) {
+        ws.E[g] = c;
+        ws.Es[g] = c;  // (round 0's snapshot: launch_fix skips its snap_kernel)
+    }
     uint32_t cnt = 0;
     uint64_t *list = ws.list + g * wp.cap;
     // Starts are held in lanes (lane j: list[cnt - nh + j]) and stored 64 at a
@@ -1438,6 +1443,7 @@ __global__ __launch_bounds__(256) void wwalk_kernel(const StreamTable st, const 
     flush();
     if (lane == 0) {
         ws.X[g] = c;
+        ws.Xs[g] = c;
         ws.N[g] = cnt;
         if (cnt > wp.cap) atomicAdd(&ws.flags[1], 1ull);
     }
@@ -2599,19 +2605,27 @@ __global__ __launch_bounds__(kScanBlock) void prefix_kernel(const WalkState ws, 
 // block, then lanes over its chunks -- coalesced stores, 4096 waves per GiB
 // (a thread per segment writing its ~40 chunks one after another took 18-25
 // us per GiB on 64 waves).
+// go: the fused end kernel's verdict word (finish_kernel: P[] is complete and
+// the output is due); null: the gate rule itself, with the prefix from bsum.
 __global__ __launch_bounds__(256) void emit_kernel(const StreamTable st, const WalkParams wp, const WalkState ws,
                                                    cdc_chunk_pod *out, uint64_t out_cap,
-                                                   const unsigned long long *egate, uint32_t egn) {
-    if (emit_skips(egate, egn)) return;
+                                                   const unsigned long long *egate, uint32_t egn,
+                                                   const uint64_t *go) {
+    if (go ? *go == 0 : emit_skips(egate, egn)) return;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * 4 + wave_id();
     if (g >= st.total_spans) return;
-    uint32_t part = 0;
-    for (uint64_t j = (g & ~(uint64_t)(kScanBlock - 1)) + lane; j < g; j += 64) part += ws.N[j];
-    part = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(part), 63);
-    const uint64_t p = ws.bsum[g / kScanBlock] + part;
+    uint64_t p;
+    if (go) {
+        p = ws.P[g];
+    } else {
+        uint32_t part = 0;
+        for (uint64_t j = (g & ~(uint64_t)(kScanBlock - 1)) + lane; j < g; j += 64) part += ws.N[j];
+        part = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(part), 63);
+        p = ws.bsum[g / kScanBlock] + part;
+        if (lane == 0) ws.P[g] = p;
+    }
     const uint32_t n = ws.N[g];
-    if (lane == 0) ws.P[g] = p;
     if (n > wp.cap || p + n > out_cap) {
         if (lane == 0) atomicAdd(&ws.flags[1], 1ull);
         return;
@@ -2632,6 +2646,63 @@ __global__ void first_kernel(const StreamTable st, const WalkState ws, uint64_t 
     if (i > st.n) return;
     const uint64_t g = i < st.n ? st.span_base[i] : st.total_spans;
     ws.first[i] = g < st.total_spans ? ws.P[g] : ws.bsum[nb];
+}
+
+// The end of a call whose first group of fix-up rounds is queued (one block,
+// replacing sum / prefix / first and two D2H copies): when the gate rule says
+// the output is due, the exclusive prefix P[g] of every segment's count and
+// first[n+1] -- into the workspace and straight into the host staging block
+// -- and the go word for emit_kernel; in every case the flag blocks copied to
+// the host block, and, when the output is due (the host then needs no more
+// rounds), the flags reset for the next call (launch_flags_init's pattern),
+// so that call launches no init kernel.  Segment counts up to kFinishMax.
+constexpr uint32_t kFinishThreads = 1024;
+constexpr uint64_t kFinishMax = 1u << 16;
+
+__global__ __launch_bounds__(kFinishThreads) void finish_kernel(const StreamTable st, const WalkState ws,
+                                                                const unsigned long long *egate, uint32_t egn,
+                                                                uint32_t rounds, uint64_t *go, uint64_t *h_first,
+                                                                uint64_t *h_flags) {
+    __shared__ uint64_t part[kFinishThreads];
+    const bool due = !emit_skips(egate, egn);
+    const uint32_t t = threadIdx.x;
+    const uint64_t S = st.total_spans;
+    if (due) {
+        // thread t owns segments [t*per, (t+1)*per): local sums, a block scan, then the prefixes
+        const uint64_t per = (S + kFinishThreads - 1) / kFinishThreads;
+        const uint64_t a = min((uint64_t)t * per, S), b = min(a + per, S);
+        uint64_t sum = 0;
+        for (uint64_t g = a; g < b; ++g) sum += ws.N[g];
+        part[t] = sum;
+        __syncthreads();
+        for (uint32_t o = 1; o < kFinishThreads; o <<= 1) {
+            const uint64_t v = t >= o ? part[t - o] : 0;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
+        }
+        uint64_t run = part[t] - sum;
+        for (uint64_t g = a; g < b; ++g) {
+            ws.P[g] = run;
+            run += ws.N[g];
+        }
+        __syncthreads();  // (every P[] written before first[] reads them)
+        const uint64_t total = part[kFinishThreads - 1];
+        for (uint64_t i = t; i <= st.n; i += kFinishThreads) {
+            const uint64_t g = i < st.n ? st.span_base[i] : S;
+            const uint64_t f = g < S ? ws.P[g] : total;
+            ws.first[i] = f;
+            h_first[i] = f;
+        }
+    }
+    if (t == 0) *go = due ? 1 : 0;
+    const uint32_t words = 4 + 4 * rounds;
+    for (uint32_t i = t; i < words; i += kFinishThreads) h_flags[i] = ws.flags[i];
+    __threadfence_system();
+    __syncthreads();
+    if (due)
+        for (uint32_t i = t; i < 4 + 4 * kMaxFixRounds; i += kFinishThreads)
+            ws.flags[i] = i >= 4 && (i & 3) == 2 ? ~0ull : 0ull;
 }
 
 template <int kAlgo, bool kBits>
@@ -2756,10 +2827,11 @@ hipError_t launch_flags_init(unsigned long long *flags, uint32_t rounds, hipStre
     return hipGetLastError();
 }
 
-hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s) {
+hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s,
+                      bool snap) {
     if (!st.total_spans) return hipSuccess;
     const uint64_t sb = (st.total_spans + 255) / 256;
-    snap_kernel<<<(unsigned)(sb < 1024 ? sb : 1024), 256, 0, s>>>(ws, st.total_spans);
+    if (snap) snap_kernel<<<(unsigned)(sb < 1024 ? sb : 1024), 256, 0, s>>>(ws, st.total_spans);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (wp.wave && wp.nbm) {
@@ -2792,9 +2864,21 @@ hipError_t launch_emit(const StreamTable &st, const WalkParams &wp, const WalkSt
         sum_kernel<<<(unsigned)nb, kScanBlock, 0, s>>>(st, ws, egate, egn);
         prefix_kernel<<<1, kScanBlock, 0, s>>>(ws, nb, egate, egn);
         emit_kernel<<<(unsigned)((st.total_spans + 3) / 4), 256, 0, s>>>(
-            st, wp, ws, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap, egate, egn);
+            st, wp, ws, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap, egate, egn, nullptr);
     }
     first_kernel<<<(unsigned)((st.n + 1 + 255) / 256), 256, 0, s>>>(st, ws, nb, egate, egn);
+    return hipGetLastError();
+}
+
+bool finish_fits(const StreamTable &st) { return st.total_spans <= kFinishMax; }
+
+hipError_t launch_finish_emit(const StreamTable &st, const WalkParams &wp, const WalkState &ws, void *d_out,
+                              uint64_t out_cap, hipStream_t s, const unsigned long long *egate, uint32_t egn,
+                              uint32_t rounds, uint64_t *go, uint64_t *h_first, uint64_t *h_flags) {
+    finish_kernel<<<1, kFinishThreads, 0, s>>>(st, ws, egate, egn, rounds, go, h_first, h_flags);
+    if (st.total_spans)
+        emit_kernel<<<(unsigned)((st.total_spans + 3) / 4), 256, 0, s>>>(
+            st, wp, ws, reinterpret_cast<cdc_chunk_pod *>(d_out), out_cap, egate, egn, go);
     return hipGetLastError();
 }
 

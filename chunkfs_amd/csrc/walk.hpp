@@ -136,10 +136,13 @@ hipError_t launch_flags_init(unsigned long long *flags, uint32_t rounds, hipStre
 // Link mode: candidate lists (wave per segment), then the links (lane per candidate).
 hipError_t launch_links(const StreamTable &st, const WalkParams &wp, hipStream_t s);
 hipError_t launch_walk(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
-// One Jacobi round: snapshot X and E (one launch), then re-walk every segment whose entry is not
-// its predecessor's exit, stopping where the new chain meets the old one.
-// flags[0] counts the re-walks that changed an exit (the host loops while > 0).
-hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
+// One Jacobi round: snapshot X and E (one launch; snap = false for round 0,
+// whose snapshot the walk itself wrote), then re-walk every segment whose
+// entry is not its predecessor's exit, stopping where the new chain meets the
+// old one.  flags[0] counts the re-walks that changed an exit (the host loops
+// while > 0).
+hipError_t launch_fix(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s,
+                      bool snap = true);
 // Exact in-order pass over all segments from the lowest one re-walked.
 hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const WalkState &ws, hipStream_t s);
 // Prefix of N, first[], and the Chunk{offset,length} output.  egate (the
@@ -149,6 +152,17 @@ hipError_t launch_serial(const StreamTable &st, const WalkParams &wp, const Walk
 hipError_t launch_emit(const StreamTable &st, const WalkParams &wp, const WalkState &ws, void *d_out,
                        uint64_t out_cap, hipStream_t s, const unsigned long long *egate = nullptr,
                        uint32_t egate_rounds = 0);
+// The same output behind the first group (egate, egate_rounds) in two
+// launches: finish_kernel (one block: the prefix of N as P[], first[] into
+// the workspace and into h_first, the go word for the gated emit, the flag
+// blocks of `rounds` rounds into h_flags, and -- when the output is due -- the
+// flags reset for the next call), then emit_kernel.  h_first / h_flags are
+// host-coherent pinned memory.  For batches of <= 2^16 segments (finish_fits).
+bool finish_fits(const StreamTable &st);
+hipError_t launch_finish_emit(const StreamTable &st, const WalkParams &wp, const WalkState &ws, void *d_out,
+                              uint64_t out_cap, hipStream_t s, const unsigned long long *egate,
+                              uint32_t egate_rounds, uint32_t rounds, uint64_t *go, uint64_t *h_first,
+                              uint64_t *h_flags);
 
 }  // namespace walk
 }  // namespace cdc
