@@ -10,7 +10,7 @@ run() {  # name, counters...  (kernel regex: $RKRE, default $KRE)
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "${RKRE:-$KRE}" --output-format csv \
       -d $OUT/$name -o p -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity --no-host-path --no-algos \
-      --no-sweep --no-config4 > $OUT/$name.log 2>&1
+      --no-sweep --no-config4 --no-config5 > $OUT/$name.log 2>&1
   local rc=$?
   echo "pmc $name rc=$rc"
   return $rc
