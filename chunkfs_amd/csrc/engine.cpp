@@ -709,8 +709,10 @@ int Engine::fast_collect(int k) {
                      d[4] / 100.0, d[5] / 100.0 / (blocks ? blocks : 1.0));
     } else if (fp_.diag & 128) {
         const double waves = b.ovl ? (double)p3::ovl::resolve_blocks(b.spans) * 4 : (double)p3::resolve_blocks(b.spans) * 8;
-        std::fprintf(stderr, "resolve phases, us per wave (meta recs settle+wait virtual-links record-links walk "
-                             "lookback(w0) out):");
+        std::fprintf(stderr, (fp_.diag & 8192) ? "resolve link passes, us per wave (records: issue trunc link; "
+                                                 "virtual: issue trunc link; -; -):"
+                                               : "resolve phases, us per wave (meta recs settle+wait virtual-links "
+                                                 "record-links walk lookback(w0) out):");
         for (int i = 0; i < p3::kStatDiagN; ++i)
             std::fprintf(stderr, " %.2f", (double)h_misc[p3::kStatDiag0 + i] / 100.0 / (waves ? waves : 1.0));
         std::fprintf(stderr, "\n");

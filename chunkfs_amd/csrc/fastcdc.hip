@@ -1031,6 +1031,9 @@ __global__ __launch_bounds__(64) void scan_tail_kernel(const StreamTable st, con
 #define CDC_WIN_RECS 768
 #endif
 constexpr int kResWaves = CDC_RES_WAVES;
+#ifndef CDC_RES_LINK_DIAG
+#define CDC_RES_LINK_DIAG 0  // per-pass link timers (experiment builds only)
+#endif
 #ifndef CDC_RES_FASTTRUNC
 #define CDC_RES_FASTTRUNC 1  // item_trunc's steady-regime test (A/B: 0)
 #endif
@@ -1738,7 +1741,7 @@ __device__ __forceinline__ uint64_t ld_nt(const uint64_t *p) {
 // at the end (one atomic per phase per block, not per wave).
 #define CDC_DIAG_T(k)                                                  \
     do {                                                               \
-        if (fp.diag & 128) {                                           \
+        if ((fp.diag & 128) && !(CDC_RES_LINK_DIAG && (fp.diag & 8192))) { \
             const uint64_t t_ = __builtin_amdgcn_s_memrealtime();       \
             dt[k] += t_ - t_prev;                                      \
             t_prev = t_;                                               \
@@ -1888,11 +1891,26 @@ __global__ CDC_RES_ATTR void resolve_kernel(const StreamTable st, const FastPara
                 uint32_t wa[13];
                 item_load(A, gear, wa);
                 for (uint32_t base = e0; base < e1; base += 64) {
+                    // (CDC_RES_LINK_DIAG builds, diag & 8192: the pass split into
+                    // issue / truncated test / link, slots 0-2 for records, 3-5 for
+                    // virtual entries; profiles/r06/r06k_*)
+                    constexpr bool kLinkDiag = CDC_RES_LINK_DIAG;
+                    uint64_t f0 = (kLinkDiag && (fp.diag & 8192)) ? __builtin_amdgcn_s_memrealtime() : 0;
                     const LinkItem B2 = link_item(W, fp, virt, base + 64 + lane, e1);
                     uint32_t wb[13];
                     item_load(B2, gear, wb);
+                    uint64_t f1 = (kLinkDiag && (fp.diag & 8192)) ? __builtin_amdgcn_s_memrealtime() : 0;
                     const uint32_t tr = (fp.diag & 4) ? kTruncNone : item_trunc(A, wa, fp, tab, tabs);
+                    if (kLinkDiag && (fp.diag & 8192)) __builtin_amdgcn_s_waitcnt(0);
+                    uint64_t f2 = (kLinkDiag && (fp.diag & 8192)) ? __builtin_amdgcn_s_memrealtime() : 0;
                     item_link(W, fp, tab, A, tr, sl2, nv);
+                    if (kLinkDiag && (fp.diag & 8192)) {
+                        const uint64_t f3 = __builtin_amdgcn_s_memrealtime();
+                        const int o = virt ? 3 : 0;
+                        dt[o] += f1 - f0;
+                        dt[o + 1] += f2 - f1;
+                        dt[o + 2] += f3 - f2;
+                    }
                     A = B2;
 #pragma unroll
                     for (int i = 0; i < 13; ++i) wa[i] = wb[i];
