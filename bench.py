@@ -27,7 +27,12 @@ external launcher WORLD_SIZE must equal --gpus.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the scan kernel (the only
 HBM-bound kernel): achieved = input bytes per launch / average scan-kernel
-duration measured with HIP events around that launch on the engine's stream.
+duration measured with HIP events around that launch on the engine's stream,
+over the synchronous calls of latency_leg (rank 0, N=1), where each scan has
+the chip to itself: the headline's two-stream schedule starts each scan while
+the previous resolve still holds CUs, so its event span includes that wait
+(reported beside it as `kernel_ms_in_pipeline`; at N > 1 the roofline uses
+it).
 `roofline.traffic` comes from a PMC file under profiles/ only when that
 file's recorded source digest equals this build's (chunkfs_amd.build).
 `cpu_baseline` times the oracle's scalar C restatement (oracle/cdc_oracle.c)
@@ -55,8 +60,8 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--settle-ms", type=float, default=60.0,
-                   help="device warm-up before the warmup steps: read-only passes over the input for this long "
-                        "(clocks ramp over the first ~20 ms of load); 0 = none")
+                   help="device warm-up before the warmup steps: untimed steps of the workload for this long "
+                        "(clocks and the two-stream schedule settle over the first ~20 ms of load); 0 = none")
     p.add_argument("--workload", choices=["stream", "batch"], default="stream",
                    help="what `value` measures: stream = config 2 per GPU (weak), batch = config 4 (strong)")
     p.add_argument("--stream-bytes", type=int, default=1 << 30)
@@ -202,17 +207,21 @@ class DeviceEngine:
         self.torch.cuda.synchronize()
 
     def settle(self, w, ms):
-        """Device warm-up before the warmup steps: read-only passes over the
-        first stream (cdc_debug_read_bw) for >= ms of wall time.  MI355X
-        clocks ramp over the first ~20 ms of load: with 3 warmup steps and no
-        settle the timed steps ran at 0.322 ms, after it at 0.276
-        (profiles/r05/r05ac_*)."""
+        """Device warm-up before the warmup steps: untimed back-to-back steps
+        of the workload for >= ms of wall time, then a drain.  MI355X clocks
+        ramp over the first tens of ms of load: with 3 warmup steps and no
+        settle the timed steps ran at 0.322 ms, after 60 ms of read-only
+        passes at 0.276 (profiles/r05/r05ac_*); the two-stream schedule's
+        step keeps falling for ~70 steps (~20 ms) of its own load whatever ran
+        before it (0.32 -> 0.255 ms, profiles/r06/r06z_*), so the settle runs
+        the workload itself.  `sustained` (>= 150 ms of timed steps) checks
+        that the figure holds."""
         if not w.lens or not w.lens[0]:
             return
         t0 = time.perf_counter()
         while (time.perf_counter() - t0) * 1e3 < ms:
-            self.read_bw(w, reps=20)
-
+            self.step(w)
+        self.sync()
 
 class StubEngine:
     def __init__(self, args, local):
@@ -294,17 +303,19 @@ def latency_leg(eng, w, reps=20):
     eng.sync()
     for _ in range(3):
         eng.sync_step(w)
-    ts = []
+    ts, scans = [], []
     for _ in range(reps):
         t0 = time.perf_counter()
         eng.sync_step(w)
         ts.append(time.perf_counter() - t0)
+        scans.append(eng.timing()["scan_ms"])  # (events on every synchronous batch)
     ts.sort()
     t = eng.timing()
     return {"definition": "one synchronous cdc_chunk_batch_device call on the headline stream(s), wall time",
             "calls": reps, "median_ms": ts[len(ts) // 2] * 1e3, "min_ms": ts[0] * 1e3,
             "GiBps_at_median": sum(w.lens) / ts[len(ts) // 2] / (1 << 30),
-            "last_call_scan_ms": t["scan_ms"], "last_call_resolve_ms": t["resolve_ms"]}
+            "last_call_scan_ms": t["scan_ms"], "last_call_resolve_ms": t["resolve_ms"],
+            "scan_ms_mean": sum(scans) / len(scans) if scans else None}
 
 
 def sustained_leg(eng, w, ms_per_step, target_ms=150.0):
@@ -1029,9 +1040,13 @@ def main(argv=None):
     e2e = bytes_rank / (ms_per_step * 1e-3) / 1e9  # per-GPU bytes / wall step time
 
     extras = {}
+    pipe_scan_ms = scan_avg_ms
     if rank == 0 and world == 1 and not args.stub and shard.lens and shard.lens[0]:
         extras["sustained"] = sustained_leg(eng, w, ms_per_step)
         extras["latency_sync"] = latency_leg(eng, w)
+        if extras["latency_sync"]["scan_ms_mean"]:
+            scan_avg_ms = extras["latency_sync"]["scan_ms_mean"]  # the scan alone (module docstring)
+            achieved = bytes_rank / (scan_avg_ms * 1e-3) / 1e9
     if rank == 0 and world == 1 and not args.stub:
         if args.hash and shard.lens[0]:
             n0 = int(first[1]) - int(first[0])
@@ -1124,6 +1139,9 @@ def main(argv=None):
                 "traffic_read_kernel": traffic_read,
                 "kernel": "scan_kernel (gear candidate scan)",
                 "kernel_ms": scan_avg_ms, "algorithmic_bytes_per_launch": bytes_rank,
+                "kernel_ms_source": ("latency_sync calls (scan alone on the chip)" if pipe_scan_ms != scan_avg_ms
+                                     else "headline steps"),
+                "kernel_ms_in_pipeline": pipe_scan_ms,
                 "achievable_GBps": read_gbs,
                 "frac_of_achievable": (achieved / read_gbs) if (achieved and read_gbs) else None,
                 "achievable_definition": "read-only reduction kernel over the same bytes in this run "
@@ -1132,7 +1150,8 @@ def main(argv=None):
                                "definition": "per-GPU input bytes / wall ms_per_step"},
             },
             "cpu_baseline": extras.pop("cpu_baseline", None),
-            "phase_ms": {"scan": scan_avg_ms, "total_device": sum(t["total_ms"] for t in tims) / len(tims),
+            "phase_ms": {"scan": pipe_scan_ms, "scan_alone": scan_avg_ms,
+                         "total_device": sum(t["total_ms"] for t in tims) / len(tims),
                          "resolve": sum(t["resolve_ms"] for t in tims) / len(tims),
                          "rewalked_spans": max(t["fixup_iterations"] for t in tims),
                          "walk_fallback_steps": max(t.get("walk_fallback_steps", 0) for t in tims)},

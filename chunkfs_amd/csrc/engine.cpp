@@ -113,7 +113,10 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         fp.mask_l_sh = fp.mask_l << fp.tshift;
         if (const char *d = std::getenv("CHUNKFS_AMD_DIAG")) fp.diag = (uint32_t)std::atoi(d);
         if (const char *v = std::getenv("CHUNKFS_AMD_EVENT_EVERY")) e->event_every_ = std::max(1, std::atoi(v));
-        if (const char *v = std::getenv("CHUNKFS_AMD_OVERLAP")) e->ovl_on_ = std::atoi(v) != 0;  // (A/B, default off)
+        if (const char *v = std::getenv("CHUNKFS_AMD_OVERLAP")) {  // (A/B; default 2)
+            e->ovl_on_ = std::atoi(v) != 0;
+            e->ovl_std_ = std::atoi(v) != 1;  // 1: the overlap kernel set (fastcdc_ovl.hip)
+        }
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
         e->small_span_log2_ = l2 > 14 ? l2 : 14;
@@ -132,7 +135,7 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         // The overlap set's resolve windows hold 384 records (11 spans): keep
         // it to sizes whose windows expect <= 256 (avg >= 8 KiB at max <= 64
         // KiB); denser records would send windows to the slow global path.
-        if (11 * (span >> (pc < 63 ? pc : 63)) > 256) e->ovl_on_ = false;
+        if (11 * (span >> (pc < 63 ? pc : 63)) > 256 && !e->ovl_std_) e->ovl_on_ = false;
         // Small-stream path (small.hip): its per-lane and per-block record
         // budgets assume sparse hits, ~2^-10 per position or rarer.
         const uint32_t pmin = (uint32_t)std::min(__builtin_popcountll(fp.mask_s), __builtin_popcountll(fp.mask_l));
@@ -230,6 +233,8 @@ Engine::~Engine() {
     for (auto &ev : scan_ev_)
         if (ev) (void)hipEventDestroy(ev);
     if (res_ev_) (void)hipEventDestroy(res_ev_);
+    for (auto &ev : res_done_)
+        if (ev) (void)hipEventDestroy(ev);
     if (res_stream_) (void)hipStreamDestroy(res_stream_);
 }
 
@@ -521,6 +526,25 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
         HIP_TRY(hipStreamCreateWithFlags(&res_stream_, hipStreamNonBlocking));
         for (auto &ev : scan_ev_) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&res_ev_, hipEventDisableTiming));
+        for (auto &ev : res_done_) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (!std::getenv("CHUNKFS_AMD_NO_PREWARM")) {
+            // The first ~100 two-stream batches of a process ran 10-20 % slower
+            // than later ones, whichever handle ran them (profiles/r06/r06y_*):
+            // the cross-stream event pattern, rehearsed once here with 4-byte
+            // fills.
+            void *d = nullptr;
+            HIP_TRY(hipMalloc(&d, 256));
+            for (int i = 0; i < 256; ++i) {
+                HIP_TRY(hipMemsetAsync(d, i, 4, s));
+                HIP_TRY(hipEventRecord(scan_ev_[i % kSlots], s));
+                HIP_TRY(hipStreamWaitEvent(res_stream_, scan_ev_[i % kSlots], 0));
+                HIP_TRY(hipMemsetAsync(static_cast<char *>(d) + 128, i, 4, res_stream_));
+                HIP_TRY(hipEventRecord(res_done_[i % 3], res_stream_));
+            }
+            HIP_TRY(hipStreamSynchronize(res_stream_));
+            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(hipFree(d));
+        }
     }
     const uint32_t sl2 = bytes <= kSmallBatch ? small_span_log2_ : span_log2_;
     uint64_t spans = 0;
@@ -627,12 +651,24 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
         // user, batch seq - kSlots, is complete -- batch seq - kHostSlots was
         // collected above (or by a drain), and resolves retire in order.
         static_assert(kSlots > kHostSlots, "device slots must outlast the host blocks");
-        if (spans) HIP_TRY(p3::ovl::launch_scan(st, fp_, d_gear_, f.cand, cp, f.d_tails, f.n_tails, num_cus_, s));
+        if (spans && ovl_std_)
+            HIP_TRY(p3::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails,
+                                    num_cus_, s));
+        else if (spans)
+            HIP_TRY(p3::ovl::launch_scan(st, fp_, d_gear_, f.cand, cp, zero_copy ? h_tails : f.d_tails, f.n_tails,
+                                         num_cus_, s));
         if (timed) HIP_TRY(hipEventRecord(ev[1], s));
         HIP_TRY(hipEventRecord(scan_ev_[slot], s));
         HIP_TRY(hipStreamWaitEvent(res_stream_, scan_ev_[slot], 0));
-        if (spans) HIP_TRY(p3::ovl::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, res_stream_));
+        if (spans && ovl_std_)
+            HIP_TRY(p3::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, res_stream_));
+        else if (spans)
+            HIP_TRY(p3::ovl::launch_resolve(st, fp_, d_gear_, f.cand, ch3_, cp, rs, d_out, out_cap, res_stream_));
         if (timed) HIP_TRY(hipEventRecord(ev[2], res_stream_));
+        // (an untimed batch's own end marker on the resolve stream, where an
+        // event costs the scans nothing: a slow collection waits for this
+        // batch, not for the later resolves already queued behind it)
+        else HIP_TRY(hipEventRecord(res_done_[seq % 3], res_stream_));
     }
     rec.live = true;
     fb_seq_ = seq + 1;
@@ -684,14 +720,18 @@ int Engine::fast_collect(int k) {
     uint64_t *h_misc = b.h + 4 * h_stage_streams_;
     {
         const volatile uint64_t *done = h_misc + p3::kStatDone;
-        const auto budget =
-            std::chrono::microseconds(std::min<uint64_t>(2000, std::max<uint64_t>(100, b.bytes / 2000000)));
+        // (two streams: a batch's resolve runs after the NEXT batch's scan, so
+        // its done word comes about a step later)
+        const uint64_t us = b.ovl ? std::min<uint64_t>(4000, std::max<uint64_t>(200, b.bytes / 1000000))
+                                  : std::min<uint64_t>(2000, std::max<uint64_t>(100, b.bytes / 2000000));
+        const auto budget = std::chrono::microseconds(us);
         const auto t_spin = std::chrono::steady_clock::now();
         while (*done == ~0ull && std::chrono::steady_clock::now() - t_spin < budget) __builtin_ia32_pause();
     }
     if (h_misc[p3::kStatDone] == ~0ull) {  // (slow batch or a failure: wait for the stream itself)
         if (b.timed) HIP_TRY(hipEventSynchronize(tev_[b.seq % kTimeRing][2]));
-        else HIP_TRY(hipStreamSynchronize(b.ovl ? res_stream_ : fb_stream_));
+        else if (b.ovl) HIP_TRY(hipEventSynchronize(res_done_[b.seq % 3]));
+        else HIP_TRY(hipStreamSynchronize(fb_stream_));
     }
     b.live = false;
     if (h_misc[p3::kStatDone] != 1 || h_misc[p3::kStatError] != 0) {
@@ -702,13 +742,15 @@ int Engine::fast_collect(int k) {
     if (fp_.diag & 64) {  // resolve block spans (100 MHz stamps -> us)
         const uint64_t *d = h_misc + p3::kStatDiag0;
         const uint64_t s0 = ~d[0], s1 = d[1], e1 = d[2], e0 = ~d[3];
-        const double blocks = (double)(b.ovl ? p3::ovl::resolve_blocks(b.spans) : p3::resolve_blocks(b.spans));
+        const double blocks =
+            (double)(b.ovl && !ovl_std_ ? p3::ovl::resolve_blocks(b.spans) : p3::resolve_blocks(b.spans));
         std::fprintf(stderr, "resolve blocks, us: scan's last block end -> first start %.2f  starts spread %.2f  "
                              "first start -> first end %.2f  -> last end %.2f  longest block %.2f  mean block %.2f\n",
                      ((double)s0 - (double)d[6]) / 100.0, (s1 - s0) / 100.0, (e0 - s0) / 100.0, (e1 - s0) / 100.0,
                      d[4] / 100.0, d[5] / 100.0 / (blocks ? blocks : 1.0));
     } else if (fp_.diag & 128) {
-        const double waves = b.ovl ? (double)p3::ovl::resolve_blocks(b.spans) * 4 : (double)p3::resolve_blocks(b.spans) * 8;
+        const double waves = b.ovl && !ovl_std_ ? (double)p3::ovl::resolve_blocks(b.spans) * 4
+                                                : (double)p3::resolve_blocks(b.spans) * 8;
         std::fprintf(stderr, (fp_.diag & 8192) ? "resolve link passes, us per wave (records: issue trunc link; "
                                                  "virtual: issue trunc link; -; -):"
                                                : "resolve phases, us per wave (meta recs settle+wait virtual-links "

@@ -260,18 +260,25 @@ class Engine {
     uint64_t fb_seq_ = 0;           // batches submitted
     hipStream_t fb_stream_ = nullptr;  // the stream of the batches in flight
     bool fb_any_ = false;           // a batch is in flight
-    bool fb_ovl_ = false;           // ... of the overlap set (resolves on res_stream_)
-    // Overlapped async batches (CHUNKFS_AMD_OVERLAP=1, where the overlap
-    // set's resolve windows fit): batch k's resolve on res_stream_, behind
-    // scan_ev_[slot k], beside batch k+1's scan; res_ev_ orders the caller's
-    // stream after them at a drain.  Off by default: measured 0.33 vs 0.278
-    // ms per 1 GiB step -- the scan is issue-bound, and the co-resident
-    // resolve slowed it from 0.217 to 0.296 ms while itself taking 0.22 ms
-    // (profiles/r06/r06a_*).
-    bool ovl_on_ = false;
+    bool fb_ovl_ = false;           // ... with their resolves on res_stream_
+    // Async batches on two streams (default, CHUNKFS_AMD_OVERLAP=2): batch k's
+    // resolve on res_stream_ behind scan_ev_[slot k], batch k+1's scan on the
+    // caller's stream right behind scan k.  A resolve block (148 KiB of LDS)
+    // and a scan block (136 KiB) never share a CU, so nothing co-resides: the
+    // next scan's blocks take each CU as its resolve block retires -- the
+    // kernel-to-kernel gaps and the resolve's ragged end leave the step
+    // (0.2557 vs 0.2744 ms sustained, profiles/r06/r06p_*).  res_ev_ orders the
+    // caller's stream after the resolves at a drain.  CHUNKFS_AMD_OVERLAP=1:
+    // the same with the overlap kernel set (fastcdc_ovl.hip, where its resolve
+    // windows fit), which co-resides and measured slower (0.33 vs 0.278 ms:
+    // the issue-bound scan slowed from 0.217 to 0.296 ms, profiles/r06/r06a_*);
+    // 0: one stream.
+    bool ovl_on_ = true;
+    bool ovl_std_ = true;   // the regular kernel set on the two streams
     hipStream_t res_stream_ = nullptr;
     hipEvent_t scan_ev_[kSlots] = {};
     hipEvent_t res_ev_ = nullptr;
+    hipEvent_t res_done_[3] = {};  // untimed batch k's resolve end on res_stream_ (slot k % 3)
     int64_t held_ = 0;              // result of the last implicit drain (drain_implicit)
     bool held_valid_ = false;
     const uint64_t *cur_tails_ = nullptr;  // this batch's: d_tails_ or the staging block's

@@ -43,7 +43,10 @@ inline size_t bstamp_bytes() { return kMaxBlocks * 8 * 8; }
 // ready[piece] (pinned, coherent).  A block starts loading once every piece
 // its bytes (and the 64 before them) lie in is ready.  ready == nullptr: the
 // bytes are complete at launch.
-constexpr uint32_t kFeedLog2 = 17;
+#ifndef CDC_FEED_LOG2
+#define CDC_FEED_LOG2 17
+#endif
+constexpr uint32_t kFeedLog2 = CDC_FEED_LOG2;
 constexpr uint32_t kFeedPieces = (uint32_t)(kMaxBytes >> kFeedLog2);
 struct Feed {
     const uint64_t *ready;  // [kFeedPieces] (device address of pinned host words), or nullptr

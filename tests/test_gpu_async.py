@@ -184,11 +184,12 @@ def test_async_implicit_drain_result_held_for_batch_sync():
     ch.close()
 
 
-@pytest.mark.parametrize("overlap", ["1", "0"])
+@pytest.mark.parametrize("overlap", ["2", "1", "0"])
 def test_async_long_burst_overlap_on_and_off(monkeypatch, overlap):
     """Twelve back-to-back batches of varying shape (every device slot and host
-    block reused several times) with the overlap set on and off: identical,
-    exact chunks."""
+    block reused several times) on two streams with the regular kernels (the
+    default), with the overlap set, and on one stream: identical, exact
+    chunks."""
     import torch
     import chunkfs_amd as c
     monkeypatch.setenv("CHUNKFS_AMD_OVERLAP", overlap)

@@ -28,7 +28,7 @@ ab)
       i=$((i+1))
       env $e timeout -k 10 300 python3 -u bench.py $HEAD > gpurun_out/${T}_v${i}_$rep.json 2> gpurun_out/${T}_v${i}_$rep.err
       rc=$?; [ $rc -eq 0 ] || { echo "variant $i ($e) rc=$rc"; tail -5 gpurun_out/${T}_v${i}_$rep.err; exit $rc; }
-      python3 -c "import json; d=json.loads(open('gpurun_out/${T}_v${i}_$rep.json').read().splitlines()[-1]); s=d['summary']; print('$i [$e] rep $rep:', round(d['value'],1), 'GiB/s', round(d['ms_per_step'],4), 'ms/step scan', round(d['phase_ms']['scan'],4), 'res', round(d['phase_ms']['resolve'],4), 'sus', round(s['sustained_ms_per_step'] or 0,4), 'lat', round(s['sync_latency_ms'] or 0,4), 'par', d.get('parity_vs_oracle'))"
+      python3 -c "import json; d=json.loads(open('gpurun_out/${T}_v${i}_$rep.json').read().splitlines()[-1]); s=d['summary']; print('$i [$e] rep $rep:', round(d['value'],1), 'GiB/s', round(d['ms_per_step'],4), 'ms/step scan', round(d['phase_ms']['scan'],4), 'alone', round(d['phase_ms'].get('scan_alone') or 0,4), 'res', round(d['phase_ms']['resolve'],4), 'sus', round(s['sustained_ms_per_step'] or 0,4), 'lat', round(s['sync_latency_ms'] or 0,4), 'par', d.get('parity_vs_oracle'))"
     done
   done ;;
 prof)
