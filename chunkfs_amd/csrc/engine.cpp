@@ -30,6 +30,7 @@ thread_local std::string g_last_error;
 #define CDC_MIN_SPAN_LOG2 16
 #endif
 constexpr uint32_t kMinSpanLog2 = CDC_MIN_SPAN_LOG2;  // 64 KiB spans at least (experiment builds may raise it)
+constexpr uint32_t kMaxSpanLog2 = 17;  // ... and at most 128 KiB unless the max chunk needs more
 
 // fastcdc 3.1.0 v2020 FastCDC::new asserts (VERIFY).
 constexpr uint32_t kMinimumMin = 64, kMinimumMax = 1048576;
@@ -119,6 +120,20 @@ int Engine::create(cdc_algo_t algo, uint32_t min, uint32_t avg, uint32_t max,
         }
         uint32_t l2 = ceil_log2(max);
         e->span_log2_ = l2 > kMinSpanLog2 ? l2 : kMinSpanLog2;
+        {
+            // Up to 128 KiB spans while a resolve window (11 spans) expects <=
+            // 384 records, half its budget (4/8/16 KiB: 352): half the scan's
+            // per-span epilogues (scan 0.222 -> 0.203 ms per GiB) and half the
+            // resolve blocks, which then leave half the CUs to the next
+            // batch's scan on the two streams (0.262 -> 0.237 ms per step,
+            // profiles/r06/r06zc_*).  (256 KiB: windows overflow to the slow
+            // global path.)
+            const uint32_t pcm = (uint32_t)__builtin_popcountll(fp.cmask);
+            while (e->span_log2_ < kMaxSpanLog2 && 11 * ((2ull << e->span_log2_) >> (pcm < 63 ? pcm : 63)) <= 384)
+                ++e->span_log2_;
+        }
+        if (const char *v = std::getenv("CHUNKFS_AMD_SPAN"))  // experiments: span log2 (>= the max's, >= 14)
+            e->span_log2_ = (uint32_t)std::max<int>(std::atoi(v), (int)std::max(l2, 14u));
         e->small_span_log2_ = l2 > 14 ? l2 : 14;
         if (const char *v = std::getenv("CHUNKFS_AMD_SMALL_SPAN")) {  // experiments: 0 = off
             const int x = std::atoi(v);
