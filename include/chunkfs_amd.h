@@ -149,10 +149,12 @@ int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
 
 /* The same batch, enqueued: returns 0 once the batch is submitted, and
  * `first` (kept by the library until then) is filled by cdc_batch_sync.
- * FastCDC batches of more than 8 MiB are enqueued back to back on the stream
- * (scan, resolve, next scan ...) with no host round trip between them, their
- * results collected later; d_streams' bytes and d_out must stay untouched
- * until cdc_batch_sync.
+ * FastCDC batches of more than 8 MiB are enqueued back to back with no host
+ * round trip between them, their results collected later: the scans on
+ * hip_stream, each resolve on a second stream of the handle behind its scan,
+ * beside the next scan (CHUNKFS_AMD_OVERLAP=0 keeps both on hip_stream);
+ * cdc_batch_sync orders hip_stream after the resolves.  d_streams' bytes and
+ * d_out must stay untouched until cdc_batch_sync.
  * Consecutive async batches of one handle must use one hip_stream (another
  * stream first completes the batches in flight).  Smaller FastCDC batches
  * and other algorithms complete inside this call (first filled on return).
