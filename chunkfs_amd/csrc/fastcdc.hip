@@ -1034,6 +1034,9 @@ constexpr int kResWaves = CDC_RES_WAVES;
 #ifndef CDC_RES_LINK_DIAG
 #define CDC_RES_LINK_DIAG 0  // per-pass link timers (experiment builds only)
 #endif
+#ifndef CDC_WALK_COOP
+#define CDC_WALK_COOP 1  // walk_window's wave-cooperative exact steps (A/B: 0)
+#endif
 #ifndef CDC_RES_FASTTRUNC
 #define CDC_RES_FASTTRUNC 1  // item_trunc's steady-regime test (A/B: 0)
 #endif
@@ -1402,6 +1405,47 @@ __device__ __forceinline__ void walk_window(ChainWin &W, const FastParams &fp, c
             go = s < L.span_end;
         }
         if (!__ballot(go)) break;
+#if CDC_WALK_COOP
+        // Exact steps, wave-cooperative: lane l + 8 j takes the next start
+        // after c_j = s_l + j max for walker l (lanes 0..7), so a run of
+        // record-free max cuts (zero-filled or constant regions) costs one
+        // memory latency per 8 chunks instead of one per chunk; the walker
+        // follows the run while each next start is the next c_j.
+        static_assert(kWalkSpans == 8, "walkers are lanes 0..7");
+        {
+            const int wl = (int)(lane & 7);
+            const uint32_t jj = lane >> 3;
+            const uint64_t c0 = __shfl(s, wl);
+            const bool g0 = __shfl(go ? 1 : 0, wl) != 0;
+            const uint64_t nw = __shfl(L.n, wl);
+            const uint32_t siw = (uint32_t)__shfl((int)L.si, wl);
+            const uint8_t *dw = reinterpret_cast<const uint8_t *>(__shfl(reinterpret_cast<uint64_t>(L.data), wl));
+            const uint64_t cj = c0 + (uint64_t)jj * fp.max;
+            uint64_t nx = 0;
+            uint32_t lrj = 0;
+            if (g0 && cj < nw) nx = win_next<false>(W, fp, tab, dw, nw, siw, cj, win_lower(W, skey(siw) | cj), 0, &lrj);
+            bool run = go;
+            uint64_t cur = s;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t n_j = __shfl(nx, wl + 8 * j);
+                const uint32_t l_j = (uint32_t)__shfl((int)lrj, wl + 8 * j);
+                if (run) {
+                    ++steps;
+                    const uint64_t c_next = cur + fp.max;
+                    if (j < 7 && l_j == 0 && n_j == c_next && c_next < L.span_end) {
+                        emit_start(W, ch, L, lane, c_next, cnt, entry);  // (the run goes on from c_next)
+                        cur = c_next;
+                    } else {
+                        s = n_j;
+                        wr = l_j;
+                        go = s < L.span_end;
+                        run = false;
+                    }
+                }
+            }
+        }
+#else
         if (go) {
             ++steps;
             uint32_t lr;
@@ -1409,6 +1453,7 @@ __device__ __forceinline__ void walk_window(ChainWin &W, const FastParams &fp, c
             wr = lr;
             go = s < L.span_end;
         }
+#endif
     }
     if (cnt == 0) entry = s;
     exit = s;

@@ -341,3 +341,38 @@ def test_dma_scan_variant_bit_exact(sizes, monkeypatch):
     streams.append(np.tile(oracle.splitmix64_bytes(61, 5), 40000)[: 2 * (1 << 20) + 5])
     for data in streams:
         assert_same(ch.chunk_array(data), oracle.fastcdc(data, *sizes), f"dma {sizes} n={len(data)}")
+
+
+@pytest.mark.parametrize("sizes", [(4096, 8192, 16384), (8192, 16384, 32768)])
+def test_large_streams_max_cut_runs(sizes):
+    """Streams past the 8 MiB small-batch line take the big-span pipeline
+    (128 KiB spans at these sizes): zero runs of every length -- shorter than
+    one max chunk, a few max chunks, longer than a span and than a walk
+    window -- between random stretches, a constant run of another byte and a
+    61-byte period.  The resolve's exact steps then run as wave-cooperative
+    max-cut runs (walk_window, CDC_WALK_COOP) that must stop exactly where a
+    record or a truncated-region hit takes over.  Synchronous and async."""
+    import torch
+    import chunkfs_amd as c
+    rng = np.random.default_rng(4242)
+    parts = []
+    for k, run in enumerate([100, 5000, 16384, 40000, 131072, 300000, 1 << 20, 3 << 20, 7777, 262144 + 13]):
+        parts.append(oracle.splitmix64_bytes(int(rng.integers(1000, 200000)), 500 + k))
+        parts.append(np.zeros(run, dtype=np.uint8) if k % 3 else np.full(run, 0xA5, dtype=np.uint8))
+    parts.append(np.tile(oracle.splitmix64_bytes(61, 7), 40000))
+    parts.append(oracle.splitmix64_bytes(3 << 20, 77))
+    data = np.concatenate(parts)
+    assert len(data) > 8 << 20
+    ch = c.FastChunker(c.SizeParams(*sizes))
+    ref = oracle.fastcdc(data, *sizes)
+    out, first = _torch_batch(ch, [data])
+    assert_same(out[first[0]:first[1]], ref, f"sync {sizes}")
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(data).to(dev)
+    cap = ch.batch_max_chunks([len(data)])
+    outs = [torch.empty((cap, 2), dtype=torch.int64, device=dev) for _ in range(3)]
+    firsts = [ch.chunk_batch_device_async([buf.data_ptr()], [len(data)], o.data_ptr(), cap) for o in outs]
+    assert ch.batch_sync() == len(ref)
+    torch.cuda.synchronize()
+    for o, f in zip(outs, firsts):
+        assert_same(o.cpu().numpy().view(np.uint64)[int(f[0]):int(f[1])], ref, f"async {sizes}")
