@@ -211,9 +211,64 @@ int Engine::init() {
     return CDC_OK;
 }
 
+// A walk context and the host thread that runs its batches (Engine::walk_submit).
+struct Engine::WalkWorker {
+    Engine *ctx = nullptr;  // owned: an engine with the handle's parameters
+    int device = 0;
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    bool has_job = false, stop = false;
+    bool done = true;    // no batch posted or running
+    bool fresh = false;  // ran a batch since the last drain
+    uint64_t seq = 0;    // that batch's number
+    std::vector<const uint8_t *> ptrs;
+    std::vector<uint64_t> lens;
+    cdc_chunk_t *out = nullptr;
+    size_t cap = 0;
+    uint64_t *first = nullptr;
+    int64_t rc = 0;
+    std::string err;
+
+    void loop() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(m);
+        for (;;) {
+            cv.wait(lk, [&] { return stop || has_job; });
+            if (has_job) {  // (a stop request waits for the batch in hand)
+                has_job = false;
+                lk.unlock();
+                const int64_t r =
+                    ctx->chunk_batch_device(ptrs.size(), ptrs.data(), lens.data(), out, cap, first, nullptr);
+                std::string e = r < 0 ? std::string(last_error()) : std::string();
+                lk.lock();
+                rc = r;
+                err = std::move(e);
+                done = true;
+                cv.notify_all();
+                continue;
+            }
+            return;
+        }
+    }
+    void wait_done(std::unique_lock<std::mutex> &lk) {
+        cv.wait(lk, [&] { return done; });
+    }
+    ~WalkWorker() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();
+        delete ctx;
+    }
+};
+
 Engine::~Engine() {
     if (device_ >= 0) (void)hipSetDevice(device_);
     if (fb_any_) (void)fast_drain();
+    for (auto &w : ww_) w.reset();
     if (own_stream_) (void)hipStreamSynchronize(own_stream_);
     if (res_stream_) (void)hipStreamSynchronize(res_stream_);
     (void)hipFree(ws_);
@@ -408,6 +463,94 @@ int64_t Engine::drain_implicit() {
     return held_;
 }
 
+// Batch k of the async walk pipeline goes to context k % walk_ctx_ (2 by
+// default), once that context's previous batch is done; a failure of that batch fails this
+// call (after the other context is drained), as FastCDC's collection does.
+int64_t Engine::walk_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
+                            size_t out_cap, uint64_t *first) {
+    const int c = (int)(wk_seq_ % (uint64_t)walk_ctx_);
+    if (!ww_[c]) {
+        Engine *e = nullptr;
+        int rc = create_walk(algo_, seq_cfg_, min_, avg_, max_, device_, &e);
+        if (rc) return rc;
+        e->walk_async_ = false;
+        if (rabin_poly_) rc = e->set_rabin_poly(rabin_poly_);
+        if (rc) {
+            delete e;
+            return rc;
+        }
+        std::unique_ptr<WalkWorker> w(new WalkWorker());
+        w->ctx = e;
+        w->device = device_;
+        WalkWorker *wp = w.get();
+        w->th = std::thread([wp] { wp->loop(); });
+        ww_[c] = std::move(w);
+    }
+    WalkWorker &w = *ww_[c];
+    {
+        std::unique_lock<std::mutex> lk(w.m);
+        w.wait_done(lk);
+        if (w.fresh && w.rc < 0) {
+            const int64_t rc = w.rc;
+            const std::string msg = w.err;
+            lk.unlock();
+            (void)walk_drain();
+            set_error(msg);
+            return rc;
+        }
+        w.ptrs.assign(d_streams, d_streams + n);
+        w.lens.assign(lens, lens + n);
+        w.out = d_out;
+        w.cap = out_cap;
+        w.first = first;
+        w.seq = wk_seq_;
+        w.rc = 0;
+        w.err.clear();
+        w.done = false;
+        w.fresh = true;
+        w.has_job = true;
+    }
+    w.cv.notify_all();
+    ++wk_seq_;
+    wk_any_ = true;
+    fb_any_ = true;
+    return 0;
+}
+
+// Every walk batch in flight completed: the last one's chunk count (its
+// context's timing becomes this handle's), or the first failure.
+int64_t Engine::walk_drain() {
+    int64_t res = 0, err = 0;
+    std::string msg;
+    uint64_t last = 0;
+    bool any = false;
+    for (auto &wp : ww_) {
+        if (!wp) continue;
+        WalkWorker &w = *wp;
+        std::unique_lock<std::mutex> lk(w.m);
+        w.wait_done(lk);
+        if (!w.fresh) continue;
+        w.fresh = false;
+        if (w.rc < 0 && !err) {
+            err = w.rc;
+            msg = w.err;
+        }
+        if (!any || w.seq > last) {
+            any = true;
+            last = w.seq;
+            res = w.rc;
+            timing_ = w.ctx->timing_;
+        }
+    }
+    wk_any_ = false;
+    fb_any_ = false;
+    if (err) {
+        set_error(msg);
+        return err;
+    }
+    return res;
+}
+
 int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
                              size_t out_cap, uint64_t *first, hipStream_t stream, bool async) {
     if (n && (!d_streams || !lens || !first)) {
@@ -441,6 +584,8 @@ int64_t Engine::batch_device(size_t n, const uint8_t *const *d_streams, const ui
     }
     // FastCDC multi-megabyte batches are pipelined; everything else runs to
     // completion here, after the batches in flight.
+    if (async && is_walk() && walk_async_ && n > 0 && bytes > kSmallBatch)
+        return walk_submit(n, d_streams, lens, d_out, out_cap, first);
     const bool pipe = algo_ == CDC_ALGO_FASTCDC && n > 0 && bytes > kSmallBatch;
     if (!pipe && fb_any_) {
         const int64_t r = drain_implicit();
@@ -700,6 +845,7 @@ int64_t Engine::fast_submit(size_t n, const uint8_t *const *d_streams, const uin
 // count.
 int64_t Engine::fast_drain() {
     if (!fb_any_) return 0;
+    if (wk_any_) return walk_drain();
     const uint64_t last = fb_seq_ - 1;
     int rc = CDC_OK;
     int64_t total = 0;
@@ -1208,6 +1354,9 @@ int Engine::create_walk(cdc_algo_t algo, const uint32_t seq[4], uint32_t min, ui
         std::snprintf(buf, sizeof buf, "%s, sizes: SizeParams { min: %u, avg: %u, max: %u } [MI355X gfx950]", name,
                       min, avg, max);
     e->describe_ = buf;
+    for (int i = 0; i < 4; ++i) e->seq_cfg_[i] = seq[i];
+    if (const char *v = std::getenv("CHUNKFS_AMD_WALK_ASYNC")) e->walk_async_ = std::atoi(v) != 0;
+    if (const char *v = std::getenv("CHUNKFS_AMD_WALK_CTX")) e->walk_ctx_ = std::max(2, std::min(kWalkCtxMax, std::atoi(v)));
     int rc = e->init();
     if (rc == CDC_OK) rc = e->init_walk(seq);
     if (rc != CDC_OK) {
@@ -1361,7 +1510,13 @@ int Engine::set_rabin_poly(uint64_t P) {
         return CDC_EINVAL;
     }
     HIP_TRY(hipSetDevice(device_));
+    if (fb_any_) {  // the batches in flight finish with the polynomial they were submitted with
+        const int64_t r = drain_implicit();
+        if (r < 0) return (int)r;
+    }
     HIP_TRY(hipStreamSynchronize(own_stream_));
+    rabin_poly_ = P;
+    for (auto &w : ww_) w.reset();  // (the contexts are made again, with this polynomial)
     // The degree decides the bitmap kernel and whether it writes the quiet-run
     // summary (walk::bits_write_summary): the workspace is laid out again.
     (void)hipFree(wws_);

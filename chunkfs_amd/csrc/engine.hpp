@@ -167,6 +167,24 @@ class Engine {
     int fast_collect(int rec);
     int64_t fast_drain();
     int64_t drain_implicit();  // fast_drain for another call: its result is kept for batch_sync
+    // Async batches of the segment-walk algorithms (Rabin / Ultra / Leap /
+    // Seq): two contexts -- engines with this handle's parameters, each with
+    // its own stream and workspace -- run alternate batches synchronously,
+    // each on its own host worker thread, so one batch's walks and fix-up
+    // rounds overlap the next batch's bitmap pass on the device (a walk call
+    // keeps host logic between its kernels: the round loop).
+    int64_t walk_submit(size_t n, const uint8_t *const *d_streams, const uint64_t *lens, cdc_chunk_t *d_out,
+                        size_t out_cap, uint64_t *first);
+    int64_t walk_drain();  // fast_drain's part for these batches
+    struct WalkWorker;
+    static constexpr int kWalkCtxMax = 4;
+    std::unique_ptr<WalkWorker> ww_[kWalkCtxMax];
+    int walk_ctx_ = 2;        // contexts in use (CHUNKFS_AMD_WALK_CTX, 2..4)
+    bool wk_any_ = false;     // a walk batch is in flight
+    uint64_t wk_seq_ = 0;     // walk batches submitted
+    bool walk_async_ = true;  // CHUNKFS_AMD_WALK_ASYNC=0: walk batches complete inside the call
+    uint32_t seq_cfg_[4] = {0, 0, 0, 0};  // create_walk's SeqCDC configuration (for the contexts)
+    uint64_t rabin_poly_ = 0;             // set_rabin_poly's polynomial (0: the default), for the contexts
     // One small FastCDC stream in one launch (small.hip): CDC_OK, kSmallFallback
     // (a budget was exceeded: run the regular pipeline) or a CDC_E* code.
     static constexpr int kSmallFallback = 1;

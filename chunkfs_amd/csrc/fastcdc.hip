@@ -1034,6 +1034,9 @@ constexpr int kResWaves = CDC_RES_WAVES;
 #ifndef CDC_RES_LINK_DIAG
 #define CDC_RES_LINK_DIAG 0  // per-pass link timers (experiment builds only)
 #endif
+#ifndef CDC_RES_HOSTREL
+#define CDC_RES_HOSTREL 1  // release of the resolve's host-visible output (0 none .. 3 system fence per wave)
+#endif
 #ifndef CDC_WALK_COOP
 #define CDC_WALK_COOP 1  // walk_window's wave-cooperative exact steps (A/B: 0)
 #endif
@@ -2097,6 +2100,16 @@ __global__ CDC_RES_ATTR void resolve_kernel(const StreamTable st, const FastPara
     }
     if ((fp.diag & 128) && lane == 0)
         for (int k = 0; k < kStatDiagN; ++k) B.diag[wave][k] = dt[k];
+    // The chunk list and first[] may be coherent host memory that the host
+    // reads as soon as it sees the done word: every wave waits for its own
+    // stores before the block takes its ticket, so the last block's done
+    // word cannot overtake them.  (A system-scope fence per wave -- an L2
+    // write-back each -- cost the two-stream step 37 us.)
+#if CDC_RES_HOSTREL >= 3
+    __threadfence_system();
+#elif CDC_RES_HOSTREL >= 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t cs = 0, rw = 0, sp = 0;
@@ -2126,9 +2139,13 @@ __global__ CDC_RES_ATTR void resolve_kernel(const StreamTable st, const FastPara
         if (rw) atomicAdd((unsigned long long *)&cp.stats[kStatRewalk], (unsigned long long)rw);
         if (sp) atomicAdd((unsigned long long *)&cp.stats[kStatOnDemand], (unsigned long long)sp);
         if (err) atomicAdd((unsigned long long *)&cp.stats[kStatError], (unsigned long long)err);
+#if CDC_RES_HOSTREL >= 2
+        __threadfence_system();
+#else
         __threadfence();
+#endif
         if (atomicAdd((unsigned long long *)&cp.stats[kStatTicket], 1ull) + 1 == gridDim.x) {
-            __threadfence();
+            __threadfence_system();
             for (int i = 0; i < kStatWords; ++i)
                 if (i != kStatDone) cp.h_stats[i] = ld_agent(&cp.stats[i]);
             const uint64_t c = cp.h_stats[kStatCand];

@@ -317,8 +317,13 @@ int Engine::ensure_host_out(size_t chunks) {
     d_hout_ = nullptr;
     h_out_cap_ = 0;
     const size_t want = round_up(chunks + chunks / 8 + 64, 4096);
+    // Coherent: the host reads the chunk list as soon as the kernel's done
+    // word says so, with no stream synchronisation in between; in plain mapped
+    // memory the device's writes did not always reach lines the CPU had read
+    // in the previous call (9 of 27k calls returned a stale last chunk,
+    // tools/tails_repro.py).
     HIP_TRY(placement().host_malloc(reinterpret_cast<void **>(&h_out_), want * sizeof(cdc_chunk_t),
-                                    hipHostMallocMapped));
+                                    hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_hout_), h_out_, 0));
     h_out_cap_ = want;
     return CDC_OK;

@@ -156,8 +156,13 @@ int64_t cdc_chunk_batch_device(cdc_handle_t *h, size_t n,
  * cdc_batch_sync orders hip_stream after the resolves.  d_streams' bytes and
  * d_out must stay untouched until cdc_batch_sync.
  * Consecutive async batches of one handle must use one hip_stream (another
- * stream first completes the batches in flight).  Smaller FastCDC batches
- * and other algorithms complete inside this call (first filled on return).
+ * stream first completes the batches in flight).  Rabin / Ultra / Leap / Seq
+ * batches of more than 8 MiB alternate between two internal contexts of the
+ * handle (own streams, own host worker threads), so one batch's walks run
+ * beside the next one's bitmap pass; they are complete (host-synchronised)
+ * when cdc_batch_sync returns (CHUNKFS_AMD_WALK_ASYNC=0: inside this call).
+ * Smaller batches and FSChunker complete inside this call (first filled on
+ * return).
  * Any other call on the handle first completes the batches in flight. */
 int64_t cdc_chunk_batch_device_async(cdc_handle_t *h, size_t n,
                                      const uint8_t *const *d_streams,

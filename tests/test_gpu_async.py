@@ -106,18 +106,25 @@ def test_async_small_batches_complete_in_call():
     ch.close()
 
 
-def test_async_other_algorithms_are_synchronous():
+def test_async_other_algorithms():
+    """Segment-walk batches past 8 MiB are in flight until batch_sync (two
+    internal contexts, tests/test_gpu_walk_async.py); smaller ones complete
+    inside the call."""
     import torch
     import chunkfs_amd as c
     ch = c.RabinChunker(c.SizeParams(*SIZES))
-    n = 24 << 20
-    b = _dev_stream(torch, n, 9)
-    cap = ch.batch_max_chunks([n])
-    out = torch.empty((cap, 2), dtype=torch.int64, device="cuda:0")
-    f = ch.chunk_batch_device_async([b.data_ptr()], [n], out.data_ptr(), cap)
-    got = out[:int(f[-1])].cpu().numpy().view(np.uint64)
-    ref = oracle.cdc("rabin", b[:n].cpu().numpy(), *SIZES)
-    assert got.shape == ref.shape and (got == ref).all()
+    for n, inside in ((24 << 20, False), (4 << 20, True)):
+        b = _dev_stream(torch, n, 9)
+        cap = ch.batch_max_chunks([n])
+        out = torch.empty((cap, 2), dtype=torch.int64, device="cuda:0")
+        f = ch.chunk_batch_device_async([b.data_ptr()], [n], out.data_ptr(), cap)
+        if inside:
+            assert int(f[-1]) > 0 and ch.batch_sync() == 0
+        else:
+            assert ch.batch_sync() == int(f[-1]) > 0
+        got = out[:int(f[-1])].cpu().numpy().view(np.uint64)
+        ref = oracle.cdc("rabin", b[:n].cpu().numpy(), *SIZES)
+        assert got.shape == ref.shape and (got == ref).all()
     ch.close()
 
 
