@@ -322,8 +322,11 @@ int Engine::ensure_host_out(size_t chunks) {
     // memory the device's writes did not always reach lines the CPU had read
     // in the previous call (9 of 27k calls returned a stale last chunk,
     // tools/tails_repro.py).
+#ifndef CDC_HOUT_COHERENT
+#define CDC_HOUT_COHERENT 1
+#endif
     HIP_TRY(placement().host_malloc(reinterpret_cast<void **>(&h_out_), want * sizeof(cdc_chunk_t),
-                                    hipHostMallocMapped | hipHostMallocCoherent));
+                                    hipHostMallocMapped | (CDC_HOUT_COHERENT ? hipHostMallocCoherent : 0u)));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&d_hout_), h_out_, 0));
     h_out_cap_ = want;
     return CDC_OK;

@@ -38,6 +38,9 @@ namespace cdc {
 namespace small {
 namespace {
 
+#ifndef CDC_SMALL_FEED_ACQ
+#define CDC_SMALL_FEED_ACQ 1
+#endif
 constexpr int kWaves = 8;
 constexpr int kThreads = kWaves * 64;
 constexpr uint32_t kPiece = 4096;      // bytes per wave
@@ -360,6 +363,11 @@ __global__ __launch_bounds__(kThreads, 1) void small_kernel(const uint8_t *__res
                 while (ld_sys_64(feed.ready + k) != feed.seq && ++i < kPollMax) __builtin_amdgcn_s_sleep(2);
                 if (i >= kPollMax) L.feed_ok = 0;
             }
+#if CDC_SMALL_FEED_ACQ
+            // system-scope acquire: the slot's bytes are read after their
+            // feed words, never from cache lines of the slot's earlier use
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
         }
         if (diag && blockIdx.x == 0) ws.stamp[1] = __builtin_amdgcn_s_memrealtime();
         if (diag) ws.bstamp[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime();
